@@ -1,0 +1,445 @@
+"""ed25519-consensus on MI355X -- Python host mirror of the reference's verification API.
+
+The reference (informalsystems/ed25519-consensus 2.1.0) is Rust; no Rust toolchain exists in
+this image, so the host side above the C ABI (include/edc.h, built as csrc/libedc.so) is this
+module plus the C++ header csrc/edc.hpp. Names, argument meaning and error behaviour follow the
+reference:
+
+    reference                                   here
+    ---------------------------------------     -------------------------------------------
+    Error::{MalformedPublicKey, InvalidSignature, InvalidSliceLength}  (src/error.rs:7-20)
+                                                 MalformedPublicKey / InvalidSignature /
+                                                 InvalidSliceLength exceptions
+    Signature (src/signature.rs)                 Signature
+    VerificationKeyBytes (src/verification_key.rs:32-87)      VerificationKeyBytes
+    VerificationKey::try_from / verify (:160-258)            VerificationKey
+    batch::Item, Item::verify_single (src/batch.rs:75-107)   batch.Item
+    batch::Verifier::{new, queue, verify} (:110-217)         batch.Verifier
+    SigningKey (src/signing_key.rs; test-data source)        SigningKey
+
+All arithmetic runs in hand-written gfx950 kernels. There is NO CPU fallback: importing works
+without a GPU (so the ABI can be inspected), but any verification call raises if the HIP
+library or a GPU is missing.
+"""
+import ctypes
+import os
+import secrets
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libedc.so")
+
+EDC_OK = 0
+EDC_INVALID_SIGNATURE = 1
+EDC_MALFORMED_PUBLIC_KEY = 2
+
+# every symbol include/edc.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = [
+    "edc_device_count", "edc_create", "edc_destroy", "edc_last_error", "edc_batch_verify",
+    "edc_batch_verify_z", "edc_batch_verify_device", "edc_batch_partial_device", "edc_combine_partials",
+    "edc_verify_each", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
+    "edc_sign_device", "edc_chacha_fill_device", "edc_set_timing", "edc_last_timings", "edc_timing_name",
+    "edc_synchronize",
+]
+
+
+class Error(Exception):
+    """ed25519_consensus::Error (reference src/error.rs:7-20)."""
+
+
+class MalformedSecretKey(Error):
+    pass
+
+
+class MalformedPublicKey(Error):
+    pass
+
+
+class InvalidSignature(Error):
+    pass
+
+
+class InvalidSliceLength(Error):
+    pass
+
+
+class EngineError(RuntimeError):
+    """HIP/runtime failure. Never interpreted as a verification verdict."""
+
+
+_CODE_TO_ERR = {EDC_INVALID_SIGNATURE: InvalidSignature, EDC_MALFORMED_PUBLIC_KEY: MalformedPublicKey}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path=None):
+    """Load csrc/libedc.so and declare argument types. Raises if it is missing."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise EngineError(f"HIP extension not built: {p} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(p)
+        c_sz, c_u8p, c_u64p, c_vp = ctypes.c_size_t, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
+        lib.edc_device_count.restype = ctypes.c_int
+        lib.edc_create.restype = c_vp
+        lib.edc_create.argtypes = [ctypes.c_int]
+        lib.edc_destroy.argtypes = [c_vp]
+        lib.edc_last_error.restype = ctypes.c_char_p
+        lib.edc_last_error.argtypes = [c_vp]
+        lib.edc_batch_verify.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp]
+        lib.edc_batch_verify_z.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp]
+        lib.edc_batch_verify_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp, c_vp]
+        lib.edc_batch_partial_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
+                                                 c_vp, ctypes.POINTER(ctypes.c_int)]
+        lib.edc_combine_partials.argtypes = [c_vp, c_sz, c_u8p, ctypes.c_int, c_vp]
+        lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
+        lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
+        lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
+        lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]
+        lib.edc_sign.argtypes = [c_vp, c_sz, c_u8p, c_sz, c_vp, c_u8p, c_u64p, c_vp, c_vp]
+        lib.edc_sign_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]
+        lib.edc_chacha_fill_device.argtypes = [c_vp, c_u8p, ctypes.c_uint64, ctypes.c_uint64, c_vp]
+        lib.edc_set_timing.argtypes = [c_vp, ctypes.c_int]
+        lib.edc_last_timings.restype = ctypes.c_int
+        lib.edc_last_timings.argtypes = [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        lib.edc_timing_name.restype = ctypes.c_char_p
+        lib.edc_timing_name.argtypes = [ctypes.c_int]
+        lib.edc_synchronize.argtypes = [c_vp]
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def _arena(msgs):
+    """Flatten messages into (arena bytes, uint64 offsets[n+1])."""
+    offs = (ctypes.c_uint64 * (len(msgs) + 1))()
+    total = 0
+    for i, m in enumerate(msgs):
+        offs[i] = total
+        total += len(m)
+    offs[len(msgs)] = total
+    return b"".join(bytes(m) for m in msgs) or b"\0", offs
+
+
+class Engine:
+    """One C-ABI context = one GPU = one HIP stream (include/edc.h)."""
+
+    def __init__(self, device=None):
+        self.lib = load_library()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        cnt = self.lib.edc_device_count()
+        if cnt <= 0:
+            raise EngineError("no HIP device visible; the MI355X path has no CPU fallback")
+        self.device = device
+        self.ctx = self.lib.edc_create(device)
+        if not self.ctx:
+            raise EngineError(f"edc_create({device}) failed")
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self.ctx:
+            self.lib.edc_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc < 0:
+            raise EngineError(f"edc error {rc}: {self.lib.edc_last_error(self.ctx).decode()}")
+        return rc
+
+    # ---- bulk entry points (bytes in, verdicts out) ----
+    def batch_verify(self, vks, sigs, msgs, z_seed=None, z=None, want_check8=False):
+        n = len(vks)
+        arena, offs = _arena(msgs)
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            if z is not None:
+                rc = self.lib.edc_batch_verify_z(self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0", arena,
+                                                 offs, bytes(z) or b"\0", check8)
+            else:
+                rc = self.lib.edc_batch_verify(self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0", arena,
+                                               offs, bytes(z_seed), check8)
+        self._check(rc)
+        return rc, (check8.raw if check8 is not None else None)
+
+    def verify_each(self, vks, sigs, msgs):
+        n = len(vks)
+        arena, offs = _arena(msgs)
+        out = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            self._check(self.lib.edc_verify_each(self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0",
+                                                 arena, offs, out))
+        return list(out.raw[:n])
+
+    def verify_prehashed_each(self, vks, sigs, ks):
+        n = len(vks)
+        out = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            self._check(self.lib.edc_verify_prehashed_each(self.ctx, n, b"".join(vks) or b"\0",
+                                                           b"".join(sigs) or b"\0", b"".join(ks) or b"\0", out))
+        return list(out.raw[:n])
+
+    def challenge(self, vks, sigs, msgs):
+        n = len(vks)
+        arena, offs = _arena(msgs)
+        out = ctypes.create_string_buffer(max(32 * n, 1))
+        with self._lock:
+            self._check(self.lib.edc_challenge(self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0",
+                                               arena, offs, out))
+        return [out.raw[32 * i:32 * i + 32] for i in range(n)]
+
+    def decompress(self, encs):
+        n = len(encs)
+        xy = ctypes.create_string_buffer(max(64 * n, 1))
+        ok = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            self._check(self.lib.edc_decompress(self.ctx, n, b"".join(encs) or b"\0", xy, ok))
+        return [(bool(ok.raw[i]), xy.raw[64 * i:64 * i + 32], xy.raw[64 * i + 32:64 * i + 64]) for i in range(n)]
+
+    def sign(self, seeds, msgs, seed_index=None):
+        n = len(msgs)
+        arena, offs = _arena(msgs)
+        vk = ctypes.create_string_buffer(max(32 * n, 1))
+        sig = ctypes.create_string_buffer(max(64 * n, 1))
+        idx = None
+        if seed_index is not None:
+            idx = (ctypes.c_uint32 * n)(*seed_index)
+        with self._lock:
+            self._check(self.lib.edc_sign(self.ctx, n, b"".join(seeds), len(seeds), idx, arena, offs, vk, sig))
+        return [vk.raw[32 * i:32 * i + 32] for i in range(n)], [sig.raw[64 * i:64 * i + 64] for i in range(n)]
+
+    def combine_partials(self, partials, bad_any, want_check8=True):
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            rc = self._check(self.lib.edc_combine_partials(self.ctx, len(partials), b"".join(partials) or b"\0",
+                                                           1 if bad_any else 0, check8))
+        return rc, (check8.raw if check8 is not None else None)
+
+
+_default_engine = None
+_default_lock = threading.Lock()
+
+
+def default_engine():
+    global _default_engine
+    with _default_lock:
+        if _default_engine is None:
+            _default_engine = Engine()
+        return _default_engine
+
+
+# ------------------------------------------------------------------ reference types
+def _as_bytes(x, n):
+    b = bytes(x)
+    if len(b) != n:
+        raise InvalidSliceLength()
+    return b
+
+
+class Signature:
+    """reference src/signature.rs:8-62: 64 bytes R || s, not validated at parse time."""
+
+    __slots__ = ("R_bytes", "s_bytes")
+
+    def __init__(self, data):
+        b = _as_bytes(data, 64)
+        self.R_bytes, self.s_bytes = b[:32], b[32:]
+
+    def to_bytes(self):
+        return self.R_bytes + self.s_bytes
+
+    def __bytes__(self):
+        return self.to_bytes()
+
+    def __eq__(self, other):
+        return isinstance(other, Signature) and self.to_bytes() == other.to_bytes()
+
+    def __hash__(self):
+        return hash(self.to_bytes())
+
+    def __repr__(self):
+        return f"Signature(R_bytes={self.R_bytes.hex()}, s_bytes={self.s_bytes.hex()})"
+
+
+class VerificationKeyBytes:
+    """reference src/verification_key.rs:32-87: raw 32 bytes; Hash/Eq on the bytes."""
+
+    __slots__ = ("_b",)
+
+    def __init__(self, data):
+        if isinstance(data, (VerificationKeyBytes, VerificationKey)):
+            data = data.to_bytes()
+        self._b = _as_bytes(data, 32)
+
+    def to_bytes(self):
+        return self._b
+
+    def as_bytes(self):
+        return self._b
+
+    def __bytes__(self):
+        return self._b
+
+    def __eq__(self, other):
+        return isinstance(other, VerificationKeyBytes) and self._b == other._b
+
+    def __lt__(self, other):
+        return self._b < other._b
+
+    def __hash__(self):
+        return hash(self._b)
+
+    def __repr__(self):
+        return f"VerificationKeyBytes({self._b.hex()})"
+
+
+class VerificationKey:
+    """reference src/verification_key.rs:106-258. try_from decodes A on the GPU."""
+
+    __slots__ = ("A_bytes", "_engine")
+
+    def __init__(self, vkb, engine):
+        self.A_bytes = vkb
+        self._engine = engine
+
+    @classmethod
+    def try_from(cls, data, engine=None):
+        vkb = data if isinstance(data, VerificationKeyBytes) else VerificationKeyBytes(data)
+        eng = engine or default_engine()
+        ok, _, _ = eng.decompress([vkb.to_bytes()])[0]
+        if not ok:
+            raise MalformedPublicKey()
+        return cls(vkb, eng)
+
+    def to_bytes(self):
+        return self.A_bytes.to_bytes()
+
+    def verify(self, signature, msg):
+        """VerificationKey::verify (src/verification_key.rs:225-233)."""
+        sig = signature if isinstance(signature, Signature) else Signature(signature)
+        code = self._engine.verify_each([self.to_bytes()], [sig.to_bytes()], [bytes(msg)])[0]
+        if code != EDC_OK:
+            raise _CODE_TO_ERR[code]()
+
+
+class SigningKey:
+    """reference src/signing_key.rs (test-data source): seed -> key; sign on the GPU."""
+
+    __slots__ = ("seed", "_engine", "_vk")
+
+    def __init__(self, seed=None, engine=None):
+        self.seed = _as_bytes(seed, 32) if seed is not None else secrets.token_bytes(32)
+        self._engine = engine or default_engine()
+        self._vk = None
+
+    @classmethod
+    def new(cls, rng=None, engine=None):
+        seed = rng.token_bytes(32) if hasattr(rng, "token_bytes") else secrets.token_bytes(32)
+        return cls(seed, engine)
+
+    def verification_key_bytes(self):
+        if self._vk is None:
+            vks, _ = self._engine.sign([self.seed], [b""])
+            self._vk = VerificationKeyBytes(vks[0])
+        return self._vk
+
+    def sign(self, msg):
+        vks, sigs = self._engine.sign([self.seed], [bytes(msg)])
+        self._vk = VerificationKeyBytes(vks[0])
+        return Signature(sigs[0])
+
+
+class batch:  # namespace mirroring `ed25519_consensus::batch`
+    class Item:
+        """reference src/batch.rs:75-107. k = H(R||A||M) is computed at construction on the GPU
+        (Item::from), so verify_single is decoupled from the message."""
+
+        __slots__ = ("vk_bytes", "sig", "k", "_msg")
+
+        def __init__(self, vk_bytes, sig, msg, k=None):
+            self.vk_bytes = vk_bytes if isinstance(vk_bytes, VerificationKeyBytes) else VerificationKeyBytes(vk_bytes)
+            self.sig = sig if isinstance(sig, Signature) else Signature(sig)
+            self._msg = bytes(msg)
+            self.k = k
+
+        @classmethod
+        def from_tuple(cls, tup):
+            return cls(*tup)
+
+        def verify_single(self, engine=None):
+            eng = engine or default_engine()
+            if self.k is None:
+                self.k = eng.challenge([self.vk_bytes.to_bytes()], [self.sig.to_bytes()], [self._msg])[0]
+            code = eng.verify_prehashed_each([self.vk_bytes.to_bytes()], [self.sig.to_bytes()], [self.k])[0]
+            if code != EDC_OK:
+                raise _CODE_TO_ERR[code]()
+
+        @staticmethod
+        def verify_single_many(items, engine=None):
+            """Fallback for many items in ONE GPU launch; returns per-item verdict codes."""
+            eng = engine or default_engine()
+            need = [it for it in items if it.k is None]
+            if need:
+                ks = eng.challenge([it.vk_bytes.to_bytes() for it in need], [it.sig.to_bytes() for it in need],
+                                   [it._msg for it in need])
+                for it, k in zip(need, ks):
+                    it.k = k
+            return eng.verify_prehashed_each([it.vk_bytes.to_bytes() for it in items],
+                                             [it.sig.to_bytes() for it in items], [it.k for it in items])
+
+    class Verifier:
+        """reference src/batch.rs:110-217. Items are kept in queue order; grouping by key
+        bytes, hashing and the coalesced MSM run on the GPU inside verify()."""
+
+        def __init__(self, engine=None):
+            self._engine = engine
+            self._vks, self._sigs, self._msgs = [], [], []
+
+        @classmethod
+        def new(cls, engine=None):
+            return cls(engine)
+
+        @property
+        def batch_size(self):
+            return len(self._vks)
+
+        def queue(self, item, sig=None, msg=None):
+            if sig is not None:
+                item = batch.Item(item, sig, msg)
+            elif isinstance(item, tuple):
+                item = batch.Item(*item)
+            self._vks.append(item.vk_bytes.to_bytes())
+            self._sigs.append(item.sig.to_bytes())
+            self._msgs.append(item._msg)
+
+        def verify_detailed(self, rng=None):
+            """Returns (code, check8): check8 = compressed [8]*check (None when rejected before
+            the MSM). rng: a 32-byte ChaCha20 seed, an object with fill_bytes(n)/token_bytes(n),
+            or None (fresh OS randomness)."""
+            eng = self._engine or default_engine()
+            n = len(self._vks)
+            if isinstance(rng, (bytes, bytearray)) and len(rng) == 32:
+                return eng.batch_verify(self._vks, self._sigs, self._msgs, z_seed=bytes(rng), want_check8=True)
+            if rng is None:
+                return eng.batch_verify(self._vks, self._sigs, self._msgs, z_seed=secrets.token_bytes(32),
+                                        want_check8=True)
+            # gen_u128 per item in queue order (src/batch.rs:64-68)
+            draw = rng.fill_bytes if hasattr(rng, "fill_bytes") else rng.token_bytes
+            z = b"".join(bytes(draw(16)) for _ in range(n))
+            return eng.batch_verify(self._vks, self._sigs, self._msgs, z=z, want_check8=True)
+
+        def verify(self, rng=None):
+            """Verifier::verify: returns None on success, raises InvalidSignature otherwise."""
+            code, _ = self.verify_detailed(rng)
+            if code != EDC_OK:
+                raise InvalidSignature()

@@ -1,0 +1,389 @@
+// Pippenger multi-scalar multiplication for the batch equation (K4)
+//   check = [B_coeff]B + sum_keys [A_coeff]A + sum_i [z_i]R_i
+// (reference src/batch.rs:205-210, EdwardsPoint::vartime_multiscalar_mul; any exact algorithm
+// yields the same group element).
+//
+// Points p: 0 = B, 1..n = R_i (128-bit z, 8 windows, top digit unsigned up to 2^16),
+//           n+1..n+m = distinct keys (253-bit, 16 signed windows).
+// Buckets: signed radix-2^16 digits d, bucket |d| in window w. A bin = (window, slice of 256
+// consecutive buckets) = one workgroup. Entries are binned by a count / scan / scatter pass
+// (LDS-aggregated histograms, no global sort), then each bin's workgroup counting-sorts its
+// entries in LDS, accumulates one bucket per lane with 7M mixed additions, and reduces its 256
+// buckets to (sum_t (t+1) S_t, sum_t S_t). Windows combine slices; a final Horner pass joins
+// windows, multiplies by the cofactor and tests the identity (src/batch.rs:212-216).
+#include "edc_common.h"
+#include "edc_launch.h"
+
+namespace edc {
+
+constexpr int CNT_PTS_PER_BLOCK = 4096;   // points per count/scatter workgroup
+
+__device__ __forceinline__ void load_scalar(const uint32_t* scal, uint32_t p, uint32_t s[8]) {
+  const uint4* q = reinterpret_cast<const uint4*>(scal + (size_t)p * 8);
+  uint4 a = q[0], b = q[1];
+  s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
+}
+
+__global__ void __launch_bounds__(256) k_msm_count(uint32_t n, const uint32_t* __restrict__ scal,
+                                                   uint32_t* __restrict__ counts,
+                                                   const int* __restrict__ flags) {
+  __shared__ uint32_t hist[NBIN];
+  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  const uint32_t npts = 1 + n + (uint32_t)flags[FLAG_NKEYS];
+  const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
+  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
+    uint32_t p = p0 + t;
+    if (p >= npts) break;
+    uint32_t s[8];
+    load_scalar(scal, p, s);
+    const bool isR = p >= 1 && p <= n;
+    const int nwin = isR ? NWIN_Z : NWIN_FULL;
+    int carry = 0;
+    for (int w = 0; w < nwin; ++w) {
+      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
+      if (d) {
+        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+        atomicAdd(&hist[w * NSLICE + (b >> SLICE_BITS)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < NBIN; b += blockDim.x)
+    if (hist[b]) atomicAdd(&counts[b], hist[b]);
+}
+
+// exclusive scan of NBIN counts (one workgroup of 1024 lanes, 4 bins per lane)
+__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ counts,
+                                                   uint32_t* __restrict__ offsets,
+                                                   uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  uint32_t c[4], s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { c[j] = counts[4 * t + j]; s += c[j]; }
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    uint32_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    offsets[4 * t + j] = run;
+    cursor[4 * t + j] = run;
+    run += c[j];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t* __restrict__ scal,
+                                                     uint32_t* __restrict__ cursor,
+                                                     uint2* __restrict__ entries,
+                                                     const int* __restrict__ flags) {
+  __shared__ uint32_t hist[NBIN];
+  __shared__ uint32_t gbase[NBIN];
+  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  const uint32_t npts = 1 + n + (uint32_t)flags[FLAG_NKEYS];
+  const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
+  // pass 1: local ranks (recomputed in pass 2 from the same digits)
+  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
+    uint32_t p = p0 + t;
+    if (p >= npts) break;
+    uint32_t s[8];
+    load_scalar(scal, p, s);
+    const bool isR = p >= 1 && p <= n;
+    const int nwin = isR ? NWIN_Z : NWIN_FULL;
+    int carry = 0;
+    for (int w = 0; w < nwin; ++w) {
+      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
+      if (d) {
+        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+        atomicAdd(&hist[w * NSLICE + (b >> SLICE_BITS)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) {
+    uint32_t c = hist[b];
+    gbase[b] = c ? atomicAdd(&cursor[b], c) : 0u;
+    hist[b] = 0;
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
+    uint32_t p = p0 + t;
+    if (p >= npts) break;
+    uint32_t s[8];
+    load_scalar(scal, p, s);
+    const bool isR = p >= 1 && p <= n;
+    const int nwin = isR ? NWIN_Z : NWIN_FULL;
+    int carry = 0;
+    for (int w = 0; w < nwin; ++w) {
+      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
+      if (d) {
+        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+        uint32_t bin = w * NSLICE + (b >> SLICE_BITS);
+        uint32_t r = atomicAdd(&hist[bin], 1u);
+        entries[gbase[bin] + r] = make_uint2(p | (d < 0 ? 0x80000000u : 0u), b & (NSLICE - 1));
+      }
+    }
+  }
+}
+
+// ---- workgroup point reductions through LDS ----
+// weighted_sum over 256 points held one per lane in lds[0..255]:
+//   returns (sum_t t * P_t, sum_t P_t) in lane 0 (valid only there).
+// 64 lanes each fold 4 consecutive points sequentially, then one wave runs a suffix scan of the
+// 64 group totals (sum_g 4g run_g = 4 sum_{g>=1} Suf_g) and two tree sums.
+__device__ void weighted_sum_256(uint32_t* lds_a, uint32_t* lds_b, int t, ge_p3& wsum, ge_p3& tot) {
+  // lds_a holds 256 ext points; lds_b scratch for 2 x 64 ext points
+  ge_p3 res, run;
+  if (t < 64) {
+    ge_p3 P3 = ld_ext(lds_a + (4 * t + 3) * EXT_WORDS);
+    ge_p3 P2 = ld_ext(lds_a + (4 * t + 2) * EXT_WORDS);
+    ge_p3 P1 = ld_ext(lds_a + (4 * t + 1) * EXT_WORDS);
+    ge_p3 P0 = ld_ext(lds_a + (4 * t + 0) * EXT_WORDS);
+    run = ge_add(P3, P2);          // P3 + P2
+    res = ge_add(run, P3);         // 2P3 + P2
+    run = ge_add(run, P1);         // P3 + P2 + P1
+    res = ge_add(res, run);        // 3P3 + 2P2 + P1
+    run = ge_add(run, P0);
+  }
+  __syncthreads();
+  uint32_t* R = lds_b;                       // res_g
+  uint32_t* S = lds_b + 64 * EXT_WORDS;      // suffix of run_g
+  if (t < 64) { st_ext(R + t * EXT_WORDS, res); st_ext(S + t * EXT_WORDS, run); }
+  __syncthreads();
+  // inclusive suffix scan over g (Hillis-Steele, 6 steps)
+  for (int d = 1; d < 64; d <<= 1) {
+    ge_p3 other;
+    bool has = (t < 64) && (t + d < 64);
+    if (has) other = ld_ext(S + (t + d) * EXT_WORDS);
+    __syncthreads();
+    if (has) { run = ge_add(run, other); st_ext(S + t * EXT_WORDS, run); }
+    __syncthreads();
+  }
+  // run = Suf_t. Need A = sum res_g, Bs = sum_{g>=1} Suf_g ; tot = Suf_0.
+  ge_p3 a = res, b = (t >= 1) ? run : ge_identity();
+  if (t == 0) tot = run;
+  for (int d = 32; d >= 1; d >>= 1) {
+    __syncthreads();
+    if (t < 64 && t >= d && t < 2 * d) { st_ext(R + (t - d) * EXT_WORDS + 0, a); }
+    __syncthreads();
+    if (t < d) a = ge_add(a, ld_ext(R + t * EXT_WORDS));
+    __syncthreads();
+    if (t < 64 && t >= d && t < 2 * d) { st_ext(S + (t - d) * EXT_WORDS, b); }
+    __syncthreads();
+    if (t < d) b = ge_add(b, ld_ext(S + t * EXT_WORDS));
+  }
+  if (t == 0) {
+    // sum_t t P_t = sum_g res_g + 4 * sum_{g>=1} Suf_g
+    ge_p3 b4 = ge_dbl(ge_dbl(b));
+    wsum = ge_add(a, b4);
+  }
+}
+
+constexpr int BKT_CHUNK = 4096;
+
+// one workgroup per bin (window w, slice s): bucket sums S_b for b = 256 s + t + 1 and
+// W_s = sum_t (t+1) S_t, T_s = sum_t S_t
+__global__ void __launch_bounds__(256) k_msm_bucket(const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ offsets,
+                                                    const uint2* __restrict__ entries,
+                                                    const uint32_t* __restrict__ pts,
+                                                    uint32_t* __restrict__ slice_W,
+                                                    uint32_t* __restrict__ slice_T) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* lidx = smem;                               // BKT_CHUNK
+  uint32_t* lcnt = smem + BKT_CHUNK;                   // 256
+  uint32_t* lstart = lcnt + NSLICE;                    // 256
+  uint32_t* lcur = lstart + NSLICE;                    // 256
+  uint32_t* lpts = smem;                               // reused: 256 ext + 128 ext (after accumulation)
+  const int t = threadIdx.x;
+  const uint32_t bin = blockIdx.x;
+  const uint32_t E = counts[bin];
+  const uint32_t off = offsets[bin];
+  if (E == 0) {
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
+    }
+    return;
+  }
+  ge_p3 acc = ge_identity();
+  for (uint32_t c0 = 0; c0 < E; c0 += BKT_CHUNK) {
+    const uint32_t ch = min((uint32_t)BKT_CHUNK, E - c0);
+    lcnt[t] = 0;
+    __syncthreads();
+    for (uint32_t e = t; e < ch; e += 256) atomicAdd(&lcnt[entries[off + c0 + e].y], 1u);
+    __syncthreads();
+    if (t < 64) {
+      // exclusive scan of 256 counts by one wave (4 per lane)
+      uint32_t c[4], s = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { c[j] = lcnt[4 * t + j]; s += c[j]; }
+      uint32_t incl = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        uint32_t v = __shfl_up(incl, d, 64);
+        if (t >= d) incl += v;
+      }
+      uint32_t run = incl - s;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lstart[4 * t + j] = run; lcur[4 * t + j] = run; run += c[j]; }
+    }
+    __syncthreads();
+    for (uint32_t e = t; e < ch; e += 256) {
+      uint2 en = entries[off + c0 + e];
+      uint32_t pos = atomicAdd(&lcur[en.y], 1u);
+      lidx[pos] = en.x;
+    }
+    __syncthreads();
+    const uint32_t beg = lstart[t], cnt = lcnt[t];
+    for (uint32_t j = 0; j < cnt; ++j) {
+      uint32_t e = lidx[beg + j];
+      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
+      if (e >> 31) q = ge_niels_neg(q);
+      acc = ge_madd(acc, q);
+    }
+    __syncthreads();
+  }
+  st_ext(lpts + t * EXT_WORDS, acc);
+  __syncthreads();
+  ge_p3 ws, tot;
+  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, t, ws, tot);
+  if (t == 0) {
+    // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
+    st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_add(ws, tot));
+    st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+  }
+}
+
+// one workgroup per window: Win_w = sum_s W_s + 256 * sum_s s T_s
+__global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__ slice_W,
+                                                    const uint32_t* __restrict__ slice_T,
+                                                    uint32_t* __restrict__ win) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int t = threadIdx.x;
+  const uint32_t w = blockIdx.x;
+  uint32_t* lpts = smem;
+  // plain sum of W_s: fold into a weighted sum call on T, and a separate tree over W
+  st_ext(lpts + t * EXT_WORDS, ld_ext(slice_T + (size_t)(w * NSLICE + t) * EXT_WORDS));
+  __syncthreads();
+  ge_p3 ws, tot;
+  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, t, ws, tot);
+  __syncthreads();
+  // tree sum of W_s
+  ge_p3 a = ld_ext(slice_W + (size_t)(w * NSLICE + t) * EXT_WORDS);
+  for (int d = 128; d >= 1; d >>= 1) {
+    __syncthreads();
+    if (t >= d && t < 2 * d) st_ext(lpts + (t - d) * EXT_WORDS, a);
+    __syncthreads();
+    if (t < d) a = ge_add(a, ld_ext(lpts + t * EXT_WORDS));
+  }
+  if (t == 0) {
+    ge_p3 x = ws;
+    for (int k = 0; k < 8; ++k) x = ge_dbl(x, k == 7);
+    st_ext(win + (size_t)w * EXT_WORDS, ge_add(a, x));
+  }
+}
+
+__device__ __forceinline__ void ext_to_canonical_bytes(const ge_p3& P, uint8_t* out) {
+  uint32_t w[8];
+  const fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
+  for (int k = 0; k < 4; ++k) {
+    fe_to_words(*c[k], w);
+    for (int j = 0; j < 8; ++j)
+      for (int b = 0; b < 4; ++b) out[32 * k + 4 * j + b] = (uint8_t)(w[j] >> (8 * b));
+  }
+}
+
+__device__ __forceinline__ ge_p3 ext_from_canonical_bytes(const uint8_t* in) {
+  ge_p3 P;
+  fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
+  for (int k = 0; k < 4; ++k) {
+    uint32_t w[8];
+    for (int j = 0; j < 8; ++j)
+      w[j] = (uint32_t)in[32 * k + 4 * j] | ((uint32_t)in[32 * k + 4 * j + 1] << 8) |
+             ((uint32_t)in[32 * k + 4 * j + 2] << 16) | ((uint32_t)in[32 * k + 4 * j + 3] << 24);
+    *c[k] = fe_from_words(w);
+  }
+  return P;
+}
+
+// result block (device): [0] verdict, [1] bad flag, [2..] pad; bytes 16..48 check8, 48..176 partial
+__device__ void finish_point(const ge_p3& check, int bad, int want_compress, uint8_t* out) {
+  ext_to_canonical_bytes(check, out + 48);
+  ge_p3 c8 = ge_mul_by_cofactor(check);
+  bool ident = ge_is_identity(c8);
+  reinterpret_cast<int*>(out)[0] = (!bad && ident) ? 0 : 1;
+  reinterpret_cast<int*>(out)[1] = bad;
+  if (want_compress) {
+    uint32_t w[8];
+    ge_compress(c8, w);
+    for (int j = 0; j < 8; ++j)
+      for (int b = 0; b < 4; ++b) out[16 + 4 * j + b] = (uint8_t)(w[j] >> (8 * b));
+  }
+}
+
+// Horner over windows, then x8 / identity / optional compression. Single lane by design
+// (the windows are already reduced); a later round can split the doublings across lanes.
+__global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restrict__ flags,
+                            int want_compress, uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 acc = ld_ext(win + (size_t)(NWIN_FULL - 1) * EXT_WORDS);
+  for (int w = NWIN_FULL - 2; w >= 0; --w) {
+    for (int k = 0; k < WIN_BITS; ++k) acc = ge_dbl(acc, k == WIN_BITS - 1);
+    acc = ge_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
+  }
+  finish_point(acc, flags[FLAG_BAD], want_compress, out);
+}
+
+// combine G partial check points (canonical 128-byte records) from G shards
+__global__ void k_combine(uint32_t g, const uint8_t* __restrict__ partials, int bad,
+                          int want_compress, uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 acc = ge_identity();
+  for (uint32_t i = 0; i < g; ++i) acc = ge_add(acc, ext_from_canonical_bytes(partials + 128 * (size_t)i));
+  finish_point(acc, bad, want_compress, out);
+}
+
+// ---------------------------------------------------------------- launchers
+static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
+                    uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags) {
+  const uint32_t maxpts = 1 + 2 * n;
+  (void)hipMemsetAsync(counts, 0, NBIN * sizeof(uint32_t), st);
+  hipLaunchKernelGGL(k_msm_count, dim3(cdiv(maxpts, CNT_PTS_PER_BLOCK)), dim3(256), 0, st, n, scal, counts,
+                     flags);
+  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, counts, offsets, cursor);
+  hipLaunchKernelGGL(k_msm_scatter, dim3(cdiv(maxpts, CNT_PTS_PER_BLOCK)), dim3(256), 0, st, n, scal,
+                     cursor, entries, flags);
+}
+
+static const size_t kReduceLds = (size_t)(NSLICE + 128) * EXT_WORDS * sizeof(uint32_t);
+
+void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
+                       const uint2* entries, const uint32_t* pts, uint32_t* slice_W, uint32_t* slice_T) {
+  hipLaunchKernelGGL(k_msm_bucket, dim3(NBIN), dim3(256), kReduceLds, st, counts, offsets, entries, pts,
+                     slice_W, slice_T);
+}
+
+void launch_msm_tail(hipStream_t st, const uint32_t* slice_W, const uint32_t* slice_T, uint32_t* win,
+                     const int* flags, int want_compress, uint8_t* out) {
+  hipLaunchKernelGGL(k_msm_window, dim3(NWIN_FULL), dim3(256), kReduceLds, st, slice_W, slice_T, win);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, win, flags, want_compress, out);
+}
+
+void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
+                    uint8_t* out) {
+  hipLaunchKernelGGL(k_combine, dim3(1), dim3(64), 0, st, g, partials, bad, want_compress, out);
+}
+
+size_t msm_entry_capacity(uint32_t n) { return (size_t)NWIN_Z * n + (size_t)NWIN_FULL * (n + 1); }
+
+}  // namespace edc

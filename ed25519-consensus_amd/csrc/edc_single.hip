@@ -1,0 +1,247 @@
+// Per-signature kernels:
+//   k_verify_single  VerificationKey::try_from + verify_prehashed, one lane per item (K5):
+//                    the fallback after a failed batch (reference src/batch.rs:104-107,
+//                    src/verification_key.rs:160-175, :237-258)
+//   k_sign           SigningKey::from(seed) + sign (test-data source only; reference
+//                    src/signing_key.rs) -- synthetic batches are generated on the GPU
+//   k_decode         CompressedEdwardsY::decompress for the API (canonical x||y + verdict)
+#include "edc_common.h"
+#include "edc_launch.h"
+
+namespace edc {
+
+// [i]B for i = 1..8 as affine Niels, filled once per context
+__global__ void k_init_btable(uint32_t* btab) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 B = ge_basepoint();
+  ge_p3 acc = B;
+  for (int i = 0; i < 8; ++i) {
+    // to affine: x = X/Z, y = Y/Z
+    fe zi = fe_invert(acc.Z);
+    ge_p3 a;
+    a.X = fe_mul(acc.X, zi); a.Y = fe_mul(acc.Y, zi); a.Z = fe_one(); a.T = fe_mul(a.X, a.Y);
+    st_niels(btab, i, ge_to_niels_affine(a));
+    acc = ge_add(acc, B);
+  }
+}
+
+// signed radix-16 digits of a scalar < 2^255, 64 digits in [-7, 8]
+__device__ __forceinline__ void radix16(const uint32_t s[8], int8_t d[64]) {
+  int carry = 0;
+  for (int j = 0; j < 64; ++j) {
+    int v = (int)((s[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
+    if (j < 63 && v > 8) { v -= 16; carry = 1; } else { carry = 0; }
+    d[j] = (int8_t)v;
+  }
+}
+
+__device__ __forceinline__ ge_cached cached_identity() {
+  ge_cached c; c.ypx = fe_one(); c.ymx = fe_one(); c.Z = fe_one(); c.T2d = fe_zero(); return c;
+}
+
+__device__ __forceinline__ void st_cached(uint32_t* p, const ge_cached& c) {
+  st_fe(p, c.ypx); st_fe(p + 9, c.ymx); st_fe(p + 18, c.Z); st_fe(p + 27, c.T2d);
+}
+__device__ __forceinline__ ge_cached ld_cached(const uint32_t* p) {
+  ge_cached c; c.ypx = ld_fe(p); c.ymx = ld_fe(p + 9); c.Z = ld_fe(p + 18); c.T2d = ld_fe(p + 27); return c;
+}
+
+constexpr int SV_THREADS = 64;
+
+// R' = [k]P + [s]B with P's table in LDS (8 cached multiples per lane), B from btab.
+__device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const uint32_t s[8],
+                                   const uint32_t* btab, uint32_t* ltab) {
+  ge_cached c = ge_to_cached(P);
+  ge_p3 acc = P;
+  st_cached(ltab, c);
+  for (int i = 1; i < 8; ++i) {
+    acc = ge_add_cached(acc, c);
+    st_cached(ltab + i * EXT_WORDS * SV_THREADS, ge_to_cached(acc));
+  }
+  int8_t kd[64], sd[64];
+  radix16(k, kd);
+  radix16(s, sd);
+  acc = ge_identity();
+  for (int j = 63; j >= 0; --j) {
+    if (j != 63) {
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, true);
+    }
+    int a = kd[j];
+    int ai = a < 0 ? -a : a;
+    ge_cached q = ai ? ld_cached(ltab + (ai - 1) * EXT_WORDS * SV_THREADS) : cached_identity();
+    if (a < 0) q = ge_cached_neg(q);
+    acc = ge_add_cached(acc, q);
+    int b = sd[j];
+    int bi = b < 0 ? -b : b;
+    ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
+    if (b < 0) nb = ge_niels_neg(nb);
+    acc = ge_madd(acc, nb);
+  }
+  return acc;
+}
+
+// verdict codes: 0 Ok, 1 InvalidSignature, 2 MalformedPublicKey
+__global__ void __launch_bounds__(SV_THREADS) k_verify_single(uint32_t n, const uint8_t* __restrict__ vk,
+                                                              const uint8_t* __restrict__ sig,
+                                                              const uint32_t* __restrict__ kscal,
+                                                              const uint32_t* __restrict__ btab,
+                                                              uint8_t* __restrict__ verdict) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  ld_words8(vk + (size_t)i * 32, w);
+  ge_p3 A;
+  if (!ge_decompress(w, A)) { verdict[i] = 2; return; }          // try_from: MalformedPublicKey
+  uint32_t sw[8];
+  ld_words8(sig + (size_t)i * 64 + 32, sw);
+  if (!sc_is_canonical(sw)) { verdict[i] = 1; return; }          // s checked before R
+  uint32_t rw[8];
+  ld_words8(sig + (size_t)i * 64, rw);
+  ge_p3 R;
+  if (!ge_decompress(rw, R)) { verdict[i] = 1; return; }
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  ge_p3 Rp = double_scalar_mul(k, ge_neg(A), sw, btab, smem + threadIdx.x * EXT_WORDS);
+  ge_p3 d = ge_add(R, ge_neg(Rp));
+  verdict[i] = ge_is_identity(ge_mul_by_cofactor(d)) ? 0 : 1;
+}
+
+// [x]B, x < 2^256
+__device__ ge_p3 base_mul(const uint32_t x[8], const uint32_t* btab) {
+  int8_t d[64];
+  radix16(x, d);
+  ge_p3 acc = ge_identity();
+  for (int j = 63; j >= 0; --j) {
+    if (j != 63) {
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, false);
+      acc = ge_dbl(acc, true);
+    }
+    int b = d[j];
+    int bi = b < 0 ? -b : b;
+    ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
+    if (b < 0) nb = ge_niels_neg(nb);
+    acc = ge_madd(acc, nb);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void words_to_bytes32(const uint32_t w[8], uint8_t* out) {
+  for (int j = 0; j < 8; ++j)
+    for (int b = 0; b < 4; ++b) out[4 * j + b] = (uint8_t)(w[j] >> (8 * b));
+}
+
+// SigningKey::from(seed) then sign(msg): a = clamp(H(seed)[0..32]), prefix = H(seed)[32..64],
+// r = H(prefix || M), R = [r]B, k = H(R || A || M), s = r + k a. vk_out/sig_out per item.
+// When shared_key != 0 every item is signed by seed 0 (no per-item key derivation repeated).
+__global__ void __launch_bounds__(64) k_sign(uint32_t n, const uint8_t* __restrict__ seeds,
+                                             const uint32_t* __restrict__ seed_index,
+                                             const uint8_t* __restrict__ msg,
+                                             const uint64_t* __restrict__ off,
+                                             const uint32_t* __restrict__ btab,
+                                             uint8_t* __restrict__ vk_out, uint8_t* __restrict__ sig_out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t si = seed_index ? seed_index[i] : i;
+  const uint8_t* seed = seeds + (size_t)si * 32;
+  uint8_t h[64];
+  sha_src hs{seed, nullptr, nullptr, 0};
+  sha512_src(hs, h);
+  uint8_t ab[32];
+  for (int j = 0; j < 32; ++j) ab[j] = h[j];
+  ab[0] &= 248; ab[31] &= 127; ab[31] |= 64;
+  uint32_t a[8];
+  for (int j = 0; j < 8; ++j)
+    a[j] = (uint32_t)ab[4 * j] | ((uint32_t)ab[4 * j + 1] << 8) | ((uint32_t)ab[4 * j + 2] << 16) |
+           ((uint32_t)ab[4 * j + 3] << 24);
+  uint32_t Aw[8];
+  ge_compress(base_mul(a, btab), Aw);
+  uint8_t Ab[32];
+  words_to_bytes32(Aw, Ab);
+  const uint64_t o0 = off[i], o1 = off[i + 1];
+  uint8_t rd[64];
+  sha_src rs{h + 32, nullptr, msg + o0, o1 - o0};
+  sha512_src(rs, rd);
+  sc r = sc_from_digest(rd);
+  uint32_t Rw[8];
+  ge_compress(base_mul(r.v, btab), Rw);
+  uint8_t Rb[32];
+  words_to_bytes32(Rw, Rb);
+  uint8_t kd[64];
+  sha_src ks{Rb, Ab, msg + o0, o1 - o0};
+  sha512_src(ks, kd);
+  sc k = sc_from_digest(kd);
+  sc as;
+  for (int j = 0; j < 8; ++j) as.v[j] = a[j];
+  sc s = sc_add(r, sc_mul(k, as));
+  for (int j = 0; j < 32; ++j) {
+    vk_out[(size_t)i * 32 + j] = Ab[j];
+    sig_out[(size_t)i * 64 + j] = Rb[j];
+  }
+  words_to_bytes32(s.v, sig_out + (size_t)i * 64 + 32);
+}
+
+// CompressedEdwardsY::decompress: ok[i] = 1 and canonical x || y, or ok[i] = 0
+__global__ void __launch_bounds__(256) k_decode(uint32_t n, const uint8_t* __restrict__ enc,
+                                                uint8_t* __restrict__ xy, uint8_t* __restrict__ ok) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8], wx[8], wy[8];
+  ld_words8(enc + (size_t)i * 32, w);
+  ge_p3 P;
+  ok[i] = ge_decompress(w, P) ? 1 : 0;
+  fe_to_words(P.X, wx);
+  fe_to_words(P.Y, wy);
+  words_to_bytes32(wx, xy + (size_t)i * 64);
+  words_to_bytes32(wy, xy + (size_t)i * 64 + 32);
+}
+
+// ChaCha20 keystream bytes [byte_off, byte_off + len) for synthetic data (64-byte aligned start)
+__global__ void __launch_bounds__(256) k_chacha_fill(uint64_t nblocks, uint64_t blk0, uint32_t k0,
+                                                     uint32_t k1, uint32_t k2, uint32_t k3, uint32_t k4,
+                                                     uint32_t k5, uint32_t k6, uint32_t k7,
+                                                     uint32_t* __restrict__ out) {
+  uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  uint32_t key[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
+  uint32_t o[16];
+  chacha20_block(key, blk0 + b, o);
+  for (int j = 0; j < 16; ++j) out[b * 16 + j] = o[j];
+}
+
+// ---------------------------------------------------------------- launchers
+static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void launch_init_btable(hipStream_t st, uint32_t* btab) {
+  hipLaunchKernelGGL(k_init_btable, dim3(1), dim3(64), 0, st, btab);
+}
+void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
+                          const uint32_t* k, const uint32_t* btab, uint8_t* verdict) {
+  if (!n) return;
+  size_t lds = (size_t)8 * EXT_WORDS * SV_THREADS * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), lds, st, n, vk, sig, k,
+                     btab, verdict);
+}
+void launch_sign(hipStream_t st, uint32_t n, const uint8_t* seeds, const uint32_t* seed_index,
+                 const uint8_t* msg, const uint64_t* off, const uint32_t* btab, uint8_t* vk_out,
+                 uint8_t* sig_out) {
+  if (n) hipLaunchKernelGGL(k_sign, dim3(cdiv(n, 64)), dim3(64), 0, st, n, seeds, seed_index, msg, off, btab,
+                            vk_out, sig_out);
+}
+void launch_decode(hipStream_t st, uint32_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok) {
+  if (n) hipLaunchKernelGGL(k_decode, dim3(cdiv(n, 256)), dim3(256), 0, st, n, enc, xy, ok);
+}
+void launch_chacha_fill(hipStream_t st, const uint32_t key[8], uint64_t blk0, uint64_t nblocks,
+                        uint32_t* out) {
+  if (nblocks)
+    hipLaunchKernelGGL(k_chacha_fill, dim3(cdiv(nblocks, 256)), dim3(256), 0, st, nblocks, blk0,
+                       key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], out);
+}
+
+}  // namespace edc

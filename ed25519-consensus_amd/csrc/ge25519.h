@@ -1,0 +1,168 @@
+// Edwards25519 group arithmetic (twisted Edwards, a = -1) in extended coordinates on top of
+// fe25519.h. All formulas are complete (no exceptional cases), so one lane = one point with no
+// data-dependent branches except the ZIP215 decode verdict.
+//
+// Restates, for the verification path of ed25519-consensus 2.1.0:
+//   CompressedEdwardsY::decompress  (reference src/batch.rs:183-185, :190-192,
+//                                    src/verification_key.rs:166-168, :242-244)
+//   EdwardsPoint::compress / mul_by_cofactor / is_identity (src/batch.rs:212,
+//                                    src/verification_key.rs:253)
+#pragma once
+#include "fe25519.h"
+
+namespace edc {
+
+struct ge_p3 { fe X, Y, Z, T; };          // extended: x = X/Z, y = Y/Z, xy = T/Z
+struct ge_niels { fe ypx, ymx, xy2d; };   // affine Niels: (y+x, y-x, 2dxy), Z = 1
+struct ge_cached { fe ypx, ymx, Z, T2d; };// projective Niels
+
+EDC_HD ge_p3 ge_identity() {
+  ge_p3 r; r.X = fe_zero(); r.Y = fe_one(); r.Z = fe_one(); r.T = fe_zero(); return r;
+}
+
+EDC_HD ge_niels ge_niels_identity() {
+  ge_niels r; r.ypx = fe_one(); r.ymx = fe_one(); r.xy2d = fe_zero(); return r;
+}
+
+// dalek FieldElement::sqrt_ratio_i. Returns was_nonzero_square; r = nonnegative root.
+EDC_HD bool fe_sqrt_ratio_i(const fe& u, const fe& v, fe& r) {
+  fe v3 = fe_mul(fe_sqr(v), v);
+  fe v7 = fe_mul(fe_sqr(v3), v);
+  r = fe_mul(fe_mul(u, v3), fe_pow_p58(fe_mul(u, v7)));
+  fe check = fe_mul(v, fe_sqr(r));
+  fe neg_u = fe_neg(u);
+  bool correct = fe_eq(check, u);
+  bool flipped = fe_eq(check, neg_u);
+  bool flipped_i = fe_eq(check, fe_mul(neg_u, fe_sqrtm1()));
+  fe r_prime = fe_mul(fe_sqrtm1(), r);
+  r = fe_select(r, r_prime, flipped || flipped_i);
+  r = fe_select(r, fe_neg(r), fe_is_negative(r));
+  return correct || flipped;
+}
+
+// ZIP215 decode: y = bytes & (2^255-1) (NOT reduced), x from sqrt_ratio_i, negate iff bit 255.
+// Returns false iff the y coordinate is not on the curve.
+EDC_HD bool ge_decompress(const uint32_t w[8], ge_p3& P) {
+  fe Y = fe_from_words(w);
+  fe one = fe_one();
+  fe YY = fe_sqr(Y);
+  fe u = fe_sub(YY, one);
+  fe v = fe_add_c(fe_mul(YY, fe_d()), one);
+  fe X;
+  bool ok = fe_sqrt_ratio_i(u, v, X);
+  bool sign = (w[7] >> 31) != 0;
+  X = fe_select(X, fe_neg(X), sign);
+  P.X = X;
+  P.Y = fe_carry(Y);
+  P.Z = one;
+  P.T = fe_mul(X, Y);
+  return ok;
+}
+
+EDC_HD ge_niels ge_to_niels_affine(const ge_p3& P) {  // requires Z == 1
+  ge_niels n;
+  n.ypx = fe_add_c(P.Y, P.X);
+  n.ymx = fe_sub(P.Y, P.X);
+  n.xy2d = fe_mul(P.T, fe_d2());
+  return n;
+}
+
+EDC_HD ge_cached ge_to_cached(const ge_p3& P) {
+  ge_cached c;
+  c.ypx = fe_add_c(P.Y, P.X);
+  c.ymx = fe_sub(P.Y, P.X);
+  c.Z = P.Z;
+  c.T2d = fe_mul(P.T, fe_d2());
+  return c;
+}
+
+EDC_HD ge_niels ge_niels_neg(const ge_niels& n) {
+  ge_niels r; r.ypx = n.ymx; r.ymx = n.ypx; r.xy2d = fe_neg(n.xy2d); return r;
+}
+
+EDC_HD ge_cached ge_cached_neg(const ge_cached& n) {
+  ge_cached r; r.ypx = n.ymx; r.ymx = n.ypx; r.Z = n.Z; r.T2d = fe_neg(n.T2d); return r;
+}
+
+EDC_HD ge_p3 ge_neg(const ge_p3& P) {
+  ge_p3 r; r.X = fe_neg(P.X); r.Y = P.Y; r.Z = P.Z; r.T = fe_neg(P.T); return r;
+}
+
+// P + Q, Q affine Niels: 7M
+EDC_HD ge_p3 ge_madd(const ge_p3& P, const ge_niels& q) {
+  fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
+  fe C = fe_mul(P.T, q.xy2d);
+  fe D = fe_add_c(P.Z, P.Z);
+  fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  ge_p3 r;
+  r.X = fe_mul(E, F); r.Y = fe_mul(G, H); r.T = fe_mul(E, H); r.Z = fe_mul(F, G);
+  return r;
+}
+
+// P + Q, Q projective Niels: 8M
+EDC_HD ge_p3 ge_add_cached(const ge_p3& P, const ge_cached& q) {
+  fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
+  fe C = fe_mul(P.T, q.T2d);
+  fe ZZ = fe_mul(P.Z, q.Z);
+  fe D = fe_add_c(ZZ, ZZ);
+  fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  ge_p3 r;
+  r.X = fe_mul(E, F); r.Y = fe_mul(G, H); r.T = fe_mul(E, H); r.Z = fe_mul(F, G);
+  return r;
+}
+
+// P + Q both extended: 9M
+EDC_HD ge_p3 ge_add(const ge_p3& P, const ge_p3& Q) { return ge_add_cached(P, ge_to_cached(Q)); }
+
+// 2P: 4S + 4M (dalek ProjectivePoint::double through the completed form). with_t=false
+// skips T3 for chains of doublings whose T is never read.
+EDC_HD ge_p3 ge_dbl(const ge_p3& P, bool with_t = true) {
+  fe XX = fe_sqr(P.X);
+  fe YY = fe_sqr(P.Y);
+  fe ZZ = fe_sqr(P.Z);
+  fe ZZ2 = fe_add(ZZ, ZZ);
+  fe XpY2 = fe_sqr(fe_add(P.X, P.Y));
+  fe Yc = fe_add(YY, XX);
+  fe Zc = fe_sub(YY, XX);
+  fe Xc = fe_sub(XpY2, Yc);
+  fe Tc = fe_sub(ZZ2, Zc);
+  ge_p3 r;
+  r.X = fe_mul(Xc, Tc);
+  r.Y = fe_mul(Yc, Zc);
+  r.Z = fe_mul(Zc, Tc);
+  r.T = with_t ? fe_mul(Xc, Yc) : fe_zero();
+  return r;
+}
+
+EDC_HD ge_p3 ge_mul_by_cofactor(const ge_p3& P) {
+  return ge_dbl(ge_dbl(ge_dbl(P, false), false), true);
+}
+
+// dalek IsIdentity on EdwardsPoint: X == 0 and Y == Z (projective)
+EDC_HD bool ge_is_identity(const ge_p3& P) {
+  return fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+}
+
+EDC_HD void ge_compress(const ge_p3& P, uint32_t w[8]) {
+  fe zi = fe_invert(P.Z);
+  fe x = fe_mul(P.X, zi);
+  fe y = fe_mul(P.Y, zi);
+  fe_to_words(y, w);
+  w[7] |= (uint32_t)fe_is_negative(x) << 31;
+}
+
+// ed25519 basepoint B (y = 4/5, x positive)
+EDC_HD ge_p3 ge_basepoint() {
+  ge_p3 B;
+  B.X = fe_const(0x8f25d51au, 0xc9562d60u, 0x9525a7b2u, 0x692cc760u, 0xfdd6dc5cu, 0xc0a4e231u,
+                 0xcd6e53feu, 0x216936d3u);
+  B.Y = fe_const(0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u,
+                 0x66666666u, 0x66666666u);
+  B.Z = fe_one();
+  B.T = fe_mul(B.X, B.Y);
+  return B;
+}
+
+}  // namespace edc

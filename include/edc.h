@@ -1,0 +1,157 @@
+/*
+ * edc.h -- C ABI of the MI355X (gfx950) ed25519-consensus batch-verification engine.
+ *
+ * This is the drop-in boundary for ONE hot path of informalsystems/ed25519-consensus 2.1.0:
+ * ZIP215 batch verification and its per-signature fallback. Every entry point below replaces a
+ * named Rust API of the reference (file:line into the reference tree) and keeps its exact
+ * semantics: non-canonical A/R encodings accepted, s must be < l, cofactored equation, batch
+ * and single verification agree. A Rust shim binds these symbols.
+ *
+ * Conventions
+ *  - Host buffers are borrowed for the duration of the call; all calls are synchronous.
+ *  - Items are in QUEUE order. vk: n*32 bytes, sig: n*64 bytes (R || s), messages are one
+ *    arena `msg` with n+1 offsets (message i = msg[msg_off[i] .. msg_off[i+1])).
+ *  - z_i = u128::from_le_bytes(ChaCha20Rng::from_seed(z_seed) keystream[16(z_base+i) ..]),
+ *    i.e. gen_u128 (reference src/batch.rs:64-68) drawn in queue order.
+ *  - Return codes: EDC_OK / EDC_INVALID_SIGNATURE / EDC_MALFORMED_PUBLIC_KEY mirror
+ *    ed25519_consensus::Error (reference src/error.rs:7-20); negative = runtime failure
+ *    (never mapped to Ok by callers).
+ *  - One context = one GPU = one HIP stream. A context must not be used from two threads at
+ *    once; use one context per thread (or per GPU / process).
+ */
+#ifndef EDC_H
+#define EDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EDC_OK 0
+#define EDC_INVALID_SIGNATURE 1      /* Error::InvalidSignature  (src/error.rs:17) */
+#define EDC_MALFORMED_PUBLIC_KEY 2   /* Error::MalformedPublicKey (src/error.rs:14) */
+#define EDC_ERR_HIP (-1)
+#define EDC_ERR_ARG (-2)
+#define EDC_ERR_NOMEM (-3)
+
+typedef struct edc_ctx edc_ctx;
+
+/* Number of visible GPUs (hipGetDeviceCount), or a negative error. */
+int edc_device_count(void);
+
+/* Create a context bound to one GPU (its own stream, constant tables, grow-only workspace). */
+edc_ctx* edc_create(int device);
+void edc_destroy(edc_ctx* ctx);
+/* Text of the last runtime error on this context ("" if none). */
+const char* edc_last_error(const edc_ctx* ctx);
+
+/*
+ * batch::Verifier::queue (x n) + Verifier::verify(rng)
+ *   reference src/batch.rs:127-137 (queue: k = H(R||A||M), group by raw key bytes)
+ *             src/batch.rs:149-217 (verify: decode, z, coalesced MSM, [8]check == 0)
+ * Returns EDC_OK if the batch equation holds, EDC_INVALID_SIGNATURE otherwise (including any
+ * undecodable A/R or non-canonical s, as the reference). check8 (nullable) receives the
+ * compressed [8]*check point when the equation was evaluated (zeros when the batch was
+ * rejected before the MSM).
+ */
+int edc_batch_verify(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                     const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
+                     uint8_t check8[32]);
+
+/* Same, with caller-drawn z (n*16 bytes, LE u128 per item) for RNGs other than ChaCha20. */
+int edc_batch_verify_z(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                       const uint8_t* msg, const uint64_t* msg_off, const uint8_t* z,
+                       uint8_t check8[32]);
+
+/*
+ * Device-resident variant (inputs already in this GPU's HBM, e.g. torch tensors). d_z may be
+ * NULL (then z comes from z_seed at global indices z_base + i).
+ */
+int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                            const uint8_t* d_msg, const uint64_t* d_msg_off,
+                            const uint8_t z_seed[32], uint64_t z_base, const uint8_t* d_z,
+                            uint8_t check8[32]);
+
+/*
+ * Multi-GPU shard: evaluate this shard's part of the batch equation WITHOUT the cofactor /
+ * identity step. partial (128 bytes) = canonical X||Y||Z||T of the shard's check point;
+ * *bad = 1 if any item of the shard failed decoding / canonicity. Items are the shard's slice
+ * of the global queue starting at global index z_base (device pointers).
+ */
+int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                             const uint8_t* d_msg, const uint64_t* d_msg_off,
+                             const uint8_t z_seed[32], uint64_t z_base, const uint8_t* d_z,
+                             uint8_t partial[128], int* bad);
+
+/*
+ * Combine g shard partials (g*128 bytes, any order) and the OR of their bad flags into the
+ * batch verdict (src/batch.rs:212-216). check8 nullable.
+ */
+int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad_any,
+                         uint8_t check8[32]);
+
+/*
+ * VerificationKey::try_from(vk) + VerificationKey::verify(sig, msg) for each item
+ *   reference src/verification_key.rs:160-175 (try_from -> MalformedPublicKey)
+ *             src/verification_key.rs:225-258 (verify / verify_prehashed)
+ * verdicts[i] in {EDC_OK, EDC_INVALID_SIGNATURE, EDC_MALFORMED_PUBLIC_KEY}. Returns 0 or <0.
+ */
+int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                    const uint8_t* msg, const uint64_t* msg_off, uint8_t* verdicts);
+
+/*
+ * batch::Item::verify_single (reference src/batch.rs:104-107): as edc_verify_each but with the
+ * queue-time challenge k (n*32 bytes, canonical scalars) instead of the message.
+ */
+int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                              const uint8_t* k, uint8_t* verdicts);
+
+/*
+ * impl From<(VerificationKeyBytes, Signature, &M)> for batch::Item (reference src/batch.rs:82-94):
+ * k_i = Scalar::from_hash(Sha512(R_i || A_i || M_i)) as 32 canonical LE bytes per item.
+ */
+int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                  const uint8_t* msg, const uint64_t* msg_off, uint8_t* k_out);
+
+/*
+ * CompressedEdwardsY::decompress as used by VerificationKey::try_from
+ * (reference src/verification_key.rs:166-168): ok[i] = 1 and xy[i] = canonical x || y, or
+ * ok[i] = 0 when the encoding is not a curve point. Returns 0 or <0.
+ */
+int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok);
+
+/*
+ * SigningKey::from([u8;32]) + SigningKey::sign (reference src/signing_key.rs:118-150,
+ * :186-205) -- test/benchmark data source. seed_index (nullable) maps item i to seed
+ * seed_index[i] (shared validator keys); vk_out n*32, sig_out n*64.
+ */
+int edc_sign(edc_ctx* ctx, size_t n, const uint8_t* seeds, size_t nseeds, const uint32_t* seed_index,
+             const uint8_t* msg, const uint64_t* msg_off, uint8_t* vk_out, uint8_t* sig_out);
+/* Device-pointer variant of edc_sign (all pointers in this GPU's memory). */
+int edc_sign_device(edc_ctx* ctx, size_t n, const uint8_t* d_seeds, const uint32_t* d_seed_index,
+                    const uint8_t* d_msg, const uint64_t* d_msg_off, uint8_t* d_vk_out,
+                    uint8_t* d_sig_out);
+
+/* ChaCha20 keystream blocks [blk0, blk0+nblocks) of key into d_out (64 bytes each), on device. */
+int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, uint64_t nblocks,
+                           uint8_t* d_out);
+
+/*
+ * Per-phase device timings of the last batch call (HIP events on the context stream), enabled
+ * by edc_set_timing(ctx, 1). Returns the number of phases written (<= cap); names via
+ * edc_timing_name(i).
+ */
+void edc_set_timing(edc_ctx* ctx, int enable);
+int edc_last_timings(const edc_ctx* ctx, float* ms, int cap);
+const char* edc_timing_name(int i);
+
+/* Synchronize the context stream (for callers that time around device calls). */
+int edc_synchronize(edc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EDC_H */

@@ -1,0 +1,69 @@
+"""CPU: the C-ABI library loads and exports every symbol include/edc.h declares; the host
+mirror exposes the reference API surface. No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "edc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(edc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(edc):
+    lib = edc.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(lib, s), f"libedc.so does not export {s}"
+    assert sorted(edc.ABI_SYMBOLS) == syms
+
+
+def test_library_is_gfx950_code_object():
+    so = os.path.join(ROOT, "ed25519-consensus_amd", "csrc", "libedc.so")
+    blob = open(so, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_timing_names_without_gpu(edc):
+    lib = edc.load_library()
+    names = [lib.edc_timing_name(i).decode() for i in range(7)]
+    assert names[0] == "challenge_sha512" and names[-1] == "msm_window_final"
+    assert lib.edc_timing_name(99) == b""
+
+
+def test_reference_api_surface(edc):
+    # names mirror ed25519_consensus: Error variants, Signature, VerificationKey(Bytes), batch
+    for name in ["Signature", "VerificationKeyBytes", "VerificationKey", "SigningKey", "InvalidSignature",
+                 "MalformedPublicKey", "InvalidSliceLength"]:
+        assert hasattr(edc, name)
+    assert hasattr(edc.batch, "Verifier") and hasattr(edc.batch, "Item")
+    assert hasattr(edc.batch.Item, "verify_single")
+    sig = edc.Signature(bytes(range(64)))
+    assert sig.R_bytes == bytes(range(32)) and sig.to_bytes() == bytes(range(64))
+    try:
+        edc.Signature(bytes(63))
+        raise AssertionError("expected InvalidSliceLength")
+    except edc.InvalidSliceLength:
+        pass
+    try:
+        edc.VerificationKeyBytes(bytes(33))
+        raise AssertionError("expected InvalidSliceLength")
+    except edc.InvalidSliceLength:
+        pass
+    a, b = edc.VerificationKeyBytes(bytes(32)), edc.VerificationKeyBytes(bytes(32))
+    assert a == b and hash(a) == hash(b)
+
+
+def test_no_gpu_means_loud_failure(edc):
+    lib = edc.load_library()
+    if lib.edc_device_count() > 0:
+        return  # on a GPU box this check does not apply
+    try:
+        edc.Engine(0)
+        raise AssertionError("Engine must refuse to run without a GPU")
+    except edc.EngineError:
+        pass

@@ -1,0 +1,114 @@
+"""CPU: the device math headers (csrc/*.h) compiled for the host by g++ (test-only library
+tests/native/libedc_hostcheck.so) agree with the oracle -- checks the radix-2^29 lazy-bound
+arithmetic, ZIP215 decode, SHA-512, scalar mod l and ChaCha20 logic without a GPU."""
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+CSRC = os.path.join(ROOT, "ed25519-consensus_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def hc():
+    so = os.path.join(NATIVE, "libedc_hostcheck.so")
+    src = os.path.join(NATIVE, "hostcheck.cpp")
+    deps = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if not os.path.exists(so) or any(os.path.getmtime(d) > os.path.getmtime(so) for d in deps):
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-Wno-unknown-pragmas",
+                               "-I", CSRC, "-o", so, src])
+    return ctypes.CDLL(so)
+
+
+def b32(x):
+    return (x % (1 << 256)).to_bytes(32, "little")
+
+
+def test_field_ops(hc, oracle):
+    P = oracle.P
+    rnd = random.Random(7)
+    out = ctypes.create_string_buffer(64)
+    edge = [0, 1, P - 1, P, P + 1, 2**255 - 1, 2**255 - 20, 2**254, 19]
+    vals = edge + [rnd.getrandbits(255) for _ in range(400)]
+    for i, a in enumerate(vals):
+        c = vals[(i * 7 + 3) % len(vals)]
+        for op, exp in [(0, a * c), (1, a * a), (2, a + c), (3, a - c), (6, -a)]:
+            hc.hc_fe_op(op, b32(a), b32(c), out)
+            assert int.from_bytes(out.raw[:32], "little") == exp % P, (op, a, c)
+    for a in vals[:40]:
+        hc.hc_fe_op(5, b32(a), b32(0), out)
+        assert int.from_bytes(out.raw[:32], "little") == pow(a, (P - 5) // 8, P)
+        if a % P:
+            hc.hc_fe_op(4, b32(a), b32(0), out)
+            assert int.from_bytes(out.raw[:32], "little") == pow(a, P - 2, P)
+
+
+def test_lazy_bound_chains(hc, oracle):
+    P = oracle.P
+    rnd = random.Random(11)
+    out = ctypes.create_string_buffer(32)
+    for _ in range(50):
+        x, y = rnd.getrandbits(255), rnd.getrandbits(255)
+        hc.hc_fe_chain(b32(x), b32(y), 64, out)
+        for _ in range(64):
+            s = (x + y) * (y + x)
+            t = s - (x + x)
+            x, y = y, (t - y) ** 2 % P
+        assert int.from_bytes(out.raw, "little") == y % P
+
+
+def test_decompress_and_point_ops(hc, oracle):
+    from conftest import golden
+    out = ctypes.create_string_buffer(64)
+    valid = []
+    for c in golden("decode.json")["cases"]:
+        e = bytes.fromhex(c["enc"])
+        ok = hc.hc_decompress(e, out)
+        assert bool(ok) == c["ok"], c["enc"]
+        if ok:
+            assert out.raw[:32].hex() == c["x"] and out.raw[32:].hex() == c["y"]
+            valid.append(e)
+    bufs = [ctypes.create_string_buffer(32) for _ in range(4)]
+    rnd = random.Random(3)
+    for _ in range(60):
+        e1, e2 = rnd.choice(valid), rnd.choice(valid)
+        assert hc.hc_point_ops(e1, e2, *bufs)
+        P1, P2 = oracle.decompress(e1), oracle.decompress(e2)
+        assert bufs[0].raw == oracle.compress(oracle.add(P1, P2))
+        assert bufs[1].raw == oracle.compress(oracle.double(P1))
+        assert bufs[2].raw == oracle.compress(oracle.add(P1, P2))
+        assert bufs[3].raw == oracle.compress(oracle.mul_by_cofactor(P1))
+
+
+def test_sha512_challenge_scalars_chacha(hc, oracle):
+    rnd = random.Random(5)
+    out = ctypes.create_string_buffer(64)
+    for ml in [0, 1, 47, 48, 63, 64, 111, 112, 127, 128, 175, 176, 300, 1024]:
+        R, A, M = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(ml)
+        hc.hc_sha512(R, A, M, ctypes.c_uint64(ml), out)
+        assert out.raw == hashlib.sha512(R + A + M).digest()
+        hc.hc_sha512(R, None, M, ctypes.c_uint64(ml), out)
+        assert out.raw == hashlib.sha512(R + M).digest()
+        hc.hc_challenge(R, A, M, ctypes.c_uint64(ml), out)
+        assert int.from_bytes(out.raw[:32], "little") == oracle.challenge(R, A, M)
+    L = oracle.L
+    for i in range(500):
+        x = rnd.getrandbits(512) if i % 4 else (1 << 512) - 1 - rnd.getrandbits(40)
+        hc.hc_sc_reduce_wide(x.to_bytes(64, "little"), out)
+        assert int.from_bytes(out.raw[:32], "little") == x % L
+        a, c = rnd.randrange(L), rnd.randrange(L)
+        for op, exp in [(0, a * c), (1, a + c), (2, a - c), (3, (a % (1 << 128)) * c)]:
+            hc.hc_sc_op(op, b32(a), b32(c), out)
+            assert int.from_bytes(out.raw[:32], "little") == exp % L
+    for v in [0, L - 1, L, L + 1, 2**255, 2**256 - 1]:
+        assert hc.hc_sc_is_canonical(b32(v)) == (v < L)
+    for key in [bytes(32), bytes([0x33]) * 32]:
+        for ctr in [0, 1, 7, 2**32 + 1]:
+            hc.hc_chacha_block(key, ctypes.c_uint64(ctr), out)
+            assert out.raw == oracle.chacha20_block(key, ctr)
