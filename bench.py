@@ -1,0 +1,226 @@
+"""Ed25519 batch verification throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE configs[2], the 2^20-signature config the metric is quoted on):
+2^20 consensus votes per GPU from 150 validators (vote i signed by validator i mod 150),
+120-byte messages (2 SHA-512 blocks), one batch equation per step. Inputs are synthetic
+(ChaCha20 streams: keygen [0x11;32], messages [0x22;32], z [0x33;32]) and signed on the GPU,
+resident in HBM before timing starts. A step = the full hot path: SHA-512 challenges, ZIP215
+decompression, key grouping, ChaCha z + scalar coefficients, Pippenger MSM, [8]/identity.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1048576] [--keys 150] [--msg-len 120]
+  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+  (weak scaling: each rank verifies its own 2^20-signature slice of one global batch; the
+   ranks all-gather one 128-byte partial point each over RCCL and combine it.)
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+# algorithmic multiply work per unit (SURVEY.md 8(d) convention: M = 64, S = 40 v_mad_u64_u32)
+ALG_MAD_M, ALG_MAD_S = 64, 40
+DECOMP_S, DECOMP_M = 255, 22                     # ZIP215 decode + Niels conversion, per point
+ALG_MAD_DECOMP = DECOMP_S * ALG_MAD_S + DECOMP_M * ALG_MAD_M
+# peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, v_mad_u64_u32 at half lane rate (measured
+# 35.0 T/s sustained by tools/microbench/valu_rates.hip, profiles/r01_valu_rates.txt)
+PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12
+HBM_PEAK_GBS = 8000.0
+
+
+def load_pkg():
+    import importlib.util
+    d = os.path.join(ROOT, "ed25519-consensus_amd")
+    if "ed25519_consensus_amd" in sys.modules:
+        return sys.modules["ed25519_consensus_amd"]
+    spec = importlib.util.spec_from_file_location("ed25519_consensus_amd", os.path.join(d, "__init__.py"),
+                                                  submodule_search_locations=[d])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ed25519_consensus_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def chacha_device(pkg, eng, torch, key, blk0, nblocks, dev):
+    out = torch.empty(max(nblocks, 1) * 64, dtype=torch.uint8, device=dev)
+    rc = eng.lib.edc_chacha_fill_device(eng.ctx, key, blk0, nblocks, ctypes.c_void_p(out.data_ptr()))
+    eng._check(rc)
+    return out
+
+
+def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
+    """Signed synthetic votes for global queue indices [global_base, global_base + n)."""
+    seeds = chacha_device(pkg, eng, torch, bytes([0x11]) * 32, 0, (keys * 32 + 63) // 64, dev)[: keys * 32]
+    stride = (msg_len + 63) // 64 * 64
+    blocks_per_msg = stride // 64
+    raw = chacha_device(pkg, eng, torch, bytes([0x22]) * 32, global_base * blocks_per_msg, n * blocks_per_msg, dev)
+    msg = raw.view(n, stride)[:, :msg_len].contiguous().view(-1) if n else raw[:1]
+    off = torch.arange(0, n + 1, dtype=torch.int64, device=dev) * msg_len
+    idx = ((torch.arange(global_base, global_base + n, dtype=torch.int64, device=dev)) % keys).to(torch.int32)
+    vk = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=dev)
+    sig = torch.empty(max(n, 1) * 64, dtype=torch.uint8, device=dev)
+    rc = eng.lib.edc_sign_device(eng.ctx, n, ctypes.c_void_p(seeds.data_ptr()), ctypes.c_void_p(idx.data_ptr()),
+                                 ctypes.c_void_p(msg.data_ptr()), ctypes.c_void_p(off.data_ptr()),
+                                 ctypes.c_void_p(vk.data_ptr()), ctypes.c_void_p(sig.data_ptr()))
+    eng._check(rc)
+    return vk, sig, msg, off
+
+
+def cpu_baseline(n_sample, keys, msg_len):
+    """Oracle CPU restatement on the host cores, bounded sample of the same workload shape."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle_c  # C restatement of the dalek u64-backend algorithm (oracle/oracle_c.py)
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "unit": "sigs/s", "cores": 0, "kind": "port",
+                "sample": f"unavailable: {e}"}
+    return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--keys", type=int, default=150)
+    ap.add_argument("--msg-len", type=int, default=120)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 13)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    torch.zeros(1, device=dev)                     # initialise torch's HIP runtime first
+
+    pkg = load_pkg()
+    eng = pkg.Engine(local)
+    from importlib import import_module
+    sharded = import_module("ed25519_consensus_amd.sharded")
+
+    n = args.n
+    base = rank * n
+    t_gen = time.perf_counter()
+    vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen
+    zseed = bytes([0x33]) * 32
+    lib = eng.lib
+    check8 = ctypes.create_string_buffer(32)
+
+    def step():
+        if world == 1:
+            rc = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                             off.data_ptr(), zseed, 0, None, check8)
+            return eng._check(rc)
+
+        def partial(zbase):
+            part = ctypes.create_string_buffer(128)
+            bad = ctypes.c_int(0)
+            eng._check(lib.edc_batch_partial_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                                    off.data_ptr(), zseed, zbase, None, part, ctypes.byref(bad)))
+            return part.raw, bad.value
+
+        code, _ = sharded.verify_sharded(partial, lambda p, b: eng.combine_partials(p, b, want_check8=False),
+                                         sharded.torch_allgather_fn(dist, dev), rank, world, base)
+        return code
+
+    for _ in range(args.warmup):
+        code = step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    codes = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    assert all(c == 0 for c in codes), f"valid synthetic batch rejected: {codes}"
+
+    # instrumented steps (outside the timed region): per-phase HIP-event timings on the
+    # context stream, for the roofline of the dominant kernel
+    lib.edc_set_timing(eng.ctx, 1)
+    names = [lib.edc_timing_name(i).decode() for i in range(7)]
+    acc = [0.0] * 7
+    for _ in range(max(1, args.profile_steps)):
+        rc = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                         off.data_ptr(), zseed, base, None, None)
+        eng._check(rc)
+        buf = (ctypes.c_float * 7)()
+        lib.edc_last_timings(eng.ctx, buf, 7)
+        for i in range(7):
+            acc[i] += buf[i] / max(1, args.profile_steps)
+    lib.edc_set_timing(eng.ctx, 0)
+    phases = {names[i]: round(acc[i], 4) for i in range(7)}
+
+    if rank == 0:
+        total = n * world * args.steps
+        value = total / elapsed
+        ms_per_step = elapsed / args.steps * 1e3
+        dom_ms = phases["decompress_R"]
+        achieved = n * ALG_MAD_DECOMP / (dom_ms * 1e-3) / 1e12
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic_decompress_R.json")
+        if os.path.exists(tpath):
+            try:
+                t = json.load(open(tpath))
+                if t.get("n") == n:
+                    traffic = t.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_sample, args.keys, args.msg_len)
+        line = {
+            "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
+            "value": round(value, 1),
+            "unit": "sigs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32/u64 integer (GF(2^255-19), radix 2^29 limbs)",
+            "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
+            "config": {"workload": "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs",
+                       "sigs_per_gpu": n, "validators": args.keys, "msg_len": args.msg_len,
+                       "parallelism": f"shard{world}" if world > 1 else "single"},
+            "roofline": {"bound": "valu_int", "kernel": "k_decompress_R",
+                         "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),
+                         "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
+                         "traffic": traffic,
+                         "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": n,
+                         "avg_launch_ms": dom_ms},
+            "phases_ms": phases,
+            "cpu_baseline": cpu,
+            "gen_s": round(t_gen, 2),
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

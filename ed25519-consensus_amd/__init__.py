@@ -24,6 +24,7 @@ library or a GPU is missing.
 import ctypes
 import os
 import secrets
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,6 +83,7 @@ def load_library(path=None):
         p = path or LIB_PATH
         if not os.path.exists(p):
             raise EngineError(f"HIP extension not built: {p} (run __graft_entry__.build())")
+        _share_torch_hip_runtime()
         lib = ctypes.CDLL(p)
         c_sz, c_u8p, c_u64p, c_vp = ctypes.c_size_t, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
         lib.edc_device_count.restype = ctypes.c_int
@@ -112,6 +114,19 @@ def load_library(path=None):
         if path is None:
             _lib = lib
         return lib
+
+
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7). If torch is in this
+    process, pre-load exactly that file so libedc.so's DT_NEEDED libamdhip64.so.7 binds to the
+    same HIP runtime instead of /opt/rocm's copy (two runtimes in one process cannot share the
+    device). Without torch, the system ROCm runtime is used."""
+    torch = sys.modules.get("torch")
+    if torch is None:
+        return
+    cand = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
 
 
 def _arena(msgs):

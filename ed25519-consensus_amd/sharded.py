@@ -1,0 +1,47 @@
+"""Multi-GPU batch verification: one process per GPU, one batch equation.
+
+The batch equation is linear (reference src/batch.rs:150-172): with the z_i drawn from one
+ChaCha20 stream at GLOBAL queue indices, shard g's part
+    P_g = [-sum_{i in g} z_i s_i]B + sum_keys [sum_{i in g} z_i k_i]A + sum_{i in g} [z_i]R_i
+satisfies check = sum_g P_g exactly. Each rank evaluates its contiguous slice of the queue on
+its own GPU (edc_batch_partial_device) and the ranks exchange ONE 128-byte partial point each
+(all-gather; RCCL over xGMI when the group backend is nccl); every rank then combines the
+partials and applies [8] / identity (edc_combine_partials) -- bit-identical to the unsharded
+verdict and [8]*check for any number of shards.
+"""
+
+
+def shard_bounds(n_total, world):
+    """Contiguous queue slices [lo, hi) per rank."""
+    return [(n_total * r // world, n_total * (r + 1) // world) for r in range(world)]
+
+
+def verify_sharded(partial_fn, combine_fn, allgather_fn, rank, world, n_local_base):
+    """Generic driver (also used by the gloo CPU tests with oracle callbacks).
+
+    partial_fn(z_base) -> (partial_bytes_128, bad_flag) for this rank's slice
+    allgather_fn(bytes_129) -> list of per-rank bytes_129 (rank order)
+    combine_fn(list_of_partials, bad_any) -> (code, check8)
+    """
+    part, bad = partial_fn(n_local_base)
+    rec = bytes(part) + bytes([1 if bad else 0])
+    recs = allgather_fn(rec)
+    assert len(recs) == world
+    partials = [r[:128] for r in recs]
+    bad_any = any(r[128] for r in recs)
+    return combine_fn(partials, bad_any)
+
+
+def torch_allgather_fn(dist, device):
+    """all_gather of fixed 129-byte records over the default process group."""
+    import torch
+
+    def fn(rec):
+        world = dist.get_world_size()
+        t = torch.tensor(list(rec), dtype=torch.uint8, device=device)
+        out = torch.empty(world * len(rec), dtype=torch.uint8, device=device)
+        dist.all_gather_into_tensor(out, t)
+        host = out.cpu().numpy().tobytes()
+        return [host[i * len(rec):(i + 1) * len(rec)] for i in range(world)]
+
+    return fn

@@ -50,6 +50,12 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def engine(edc):
+    # GPU tests share the process with torch (device tensors): import it before the HIP
+    # library is loaded so both use one HIP runtime (see load_library()).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     eng = edc.Engine(0)
     yield eng
     eng.close()
