@@ -69,15 +69,22 @@ def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
     return vk, sig, msg, off
 
 
-def cpu_baseline(n_sample, keys, msg_len):
-    """Oracle CPU restatement on the host cores, bounded sample of the same workload shape."""
+def cpu_baseline(vk, sig, msg, n_sample, keys, msg_len):
+    """Oracle C restatement (dalek u64-backend algorithm, oracle/edc_oracle.c) on the host
+    cores: the first n_sample signatures of the SAME GPU-generated workload, one Verifier per
+    thread over equal contiguous chunks, queue (SHA-512 + grouping) + verify timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
-        import oracle_c  # C restatement of the dalek u64-backend algorithm (oracle/oracle_c.py)
+        import oracle_c
     except Exception as e:  # pragma: no cover
-        return {"value": None, "unit": "sigs/s", "cores": 0, "kind": "port",
-                "sample": f"unavailable: {e}"}
-    return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len)
+        return {"value": None, "unit": "sigs/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    n_sample = min(n_sample, vk.numel() // 32)
+    vkb = vk[: 32 * n_sample].cpu().numpy().tobytes()
+    sgb = sig[: 64 * n_sample].cpu().numpy().tobytes()
+    mb = msg[: msg_len * n_sample].cpu().numpy().tobytes()
+    data = ([vkb[32 * i:32 * i + 32] for i in range(n_sample)], [sgb[64 * i:64 * i + 64] for i in range(n_sample)],
+            [mb[msg_len * i:msg_len * (i + 1)] for i in range(n_sample)])
+    return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len, data=data)
 
 
 def main():
@@ -88,7 +95,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU per step")
     ap.add_argument("--keys", type=int, default=150)
     ap.add_argument("--msg-len", type=int, default=120)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 13)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     args = ap.parse_args()
@@ -189,7 +196,7 @@ def main():
                 traffic = None
         cpu = None
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_sample, args.keys, args.msg_len)
+            cpu = cpu_baseline(vk, sig, msg, args.cpu_sample, args.keys, args.msg_len)
         line = {
             "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
             "value": round(value, 1),

@@ -1,0 +1,103 @@
+"""ctypes wrapper of oracle/build/libedc_oracle.so (the C restatement; TEST INFRASTRUCTURE /
+CPU BASELINE ONLY -- imported by tests/ and bench.py's cpu_baseline leg, never by the product)."""
+import ctypes
+import os
+import subprocess
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "build", "libedc_oracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(HERE, "edc_oracle.c")
+        if not os.path.exists(SO) or os.path.getmtime(src) > os.path.getmtime(SO):
+            subprocess.check_call(["make", "-C", HERE], stdout=subprocess.DEVNULL)
+        L = ctypes.CDLL(SO)
+        c_sz, c_p, u64p = ctypes.c_size_t, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)
+        L.oc_batch_verify.argtypes = [c_sz, c_p, c_p, c_p, u64p, c_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.oc_batch_verify_range.argtypes = [c_sz, c_p, c_p, c_p, u64p, c_p, c_p, ctypes.c_uint64, ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        L.oc_verify.argtypes = [c_p, c_p, c_p, c_sz]
+        L.oc_combine_affine.argtypes = [c_sz, c_p, ctypes.c_void_p]
+        L.oc_baseline.restype = ctypes.c_double
+        L.oc_baseline.argtypes = [c_sz, c_p, c_p, c_p, u64p, ctypes.c_int, c_sz, ctypes.POINTER(ctypes.c_int)]
+        _lib = L
+    return _lib
+
+
+def _arena(msgs):
+    offs = (ctypes.c_uint64 * (len(msgs) + 1))()
+    t = 0
+    for i, m in enumerate(msgs):
+        offs[i] = t
+        t += len(m)
+    offs[len(msgs)] = t
+    return b"".join(msgs) or b"\0", offs
+
+
+def batch_verify(items, z_seed):
+    """(code, check8 or None) -- same contract as ed25519_ref.batch_verify_seeded."""
+    vks = b"".join(v for v, _, _ in items) or b"\0"
+    sigs = b"".join(s for _, s, _ in items) or b"\0"
+    arena, offs = _arena([bytes(m) for _, _, m in items])
+    c8 = ctypes.create_string_buffer(32)
+    ev = ctypes.c_int(0)
+    rc = lib().oc_batch_verify(len(items), vks, sigs, arena, offs, bytes(z_seed), c8, ctypes.byref(ev))
+    return rc, (c8.raw if ev.value else None)
+
+
+def shard_partial_affine(items, z_seed, z_base):
+    """This shard's check point (affine x || y, 64 bytes) and its early-reject flag."""
+    vks = b"".join(v for v, _, _ in items) or b"\0"
+    sigs = b"".join(s for _, s, _ in items) or b"\0"
+    arena, offs = _arena([bytes(m) for _, _, m in items])
+    part = ctypes.create_string_buffer(64)
+    c8 = ctypes.create_string_buffer(32)
+    rc = lib().oc_batch_verify_range(len(items), vks, sigs, arena, offs, bytes(z_seed), None, z_base, c8, part)
+    evaluated = c8.raw != bytes(32)
+    return part.raw, (not evaluated)
+
+
+def combine_affine(parts):
+    c8 = ctypes.create_string_buffer(32)
+    rc = lib().oc_combine_affine(len(parts), b"".join(parts) or b"\0", c8)
+    return rc, c8.raw
+
+
+def verify(vk, sig, msg):
+    return lib().oc_verify(vk, sig, bytes(msg) or b"\0", len(msg))
+
+
+def host_threads():
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def baseline(vks, sigs, msgs, threads=None, chunk=0):
+    """All-core CPU baseline: one Verifier per thread over equal contiguous chunks, timing
+    queue (SHA-512 + grouping) + verify like reference benches/bench.rs:42-68."""
+    threads = threads or host_threads()
+    arena, offs = _arena(msgs)
+    ok = ctypes.c_int(0)
+    secs = lib().oc_baseline(len(vks), b"".join(vks), b"".join(sigs), arena, offs, threads, chunk, ctypes.byref(ok))
+    return secs, bool(ok.value), threads
+
+
+def baseline_c3(n_sample=8192, keys=150, msg_len=120, data=None):
+    """Bounded sample of the bench workload shape (C3: repeated validator keys)."""
+    if data is None:
+        raise ValueError("pass data=(vks, sigs, msgs) sampled from the GPU-generated workload")
+    vks, sigs, msgs = data
+    threads = host_threads()
+    secs, ok, threads = baseline(vks, sigs, msgs, threads=threads)
+    return {"value": round(len(vks) / secs, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
+            "ok": ok, "seconds": round(secs, 3),
+            "sample": f"{len(vks)} sigs of the same workload ({keys} validators, {msg_len}-byte msgs), "
+                      f"one Verifier per thread over {threads} equal chunks, queue+verify timed"}
