@@ -130,8 +130,9 @@ def main():
 
     def step():
         if world == 1:
+            # Verifier::verify returns only Ok/Err: no [8]*check compression in the timed loop
             rc = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
-                                             off.data_ptr(), zseed, 0, None, check8)
+                                             off.data_ptr(), zseed, 0, None, None)
             return eng._check(rc)
 
         def partial(zbase):

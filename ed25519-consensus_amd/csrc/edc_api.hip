@@ -152,22 +152,16 @@ static inline void mark(edc_ctx* ctx, int ph) {
   if (ctx->timing) (void)hipEventRecord(ctx->ev[ph], ctx->st);
 }
 
-// Stage the host inputs into the context's device buffers.
-static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
-                  const uint64_t* msg_off) {
-  if (n && (!vk || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+// Stage the message arena + offsets (0-based) into the context's device buffers.
+static int upload_msgs(edc_ctx* ctx, size_t n, const uint8_t* msg, const uint64_t* msg_off) {
+  if (n && !msg_off) { ctx->err = "null msg_off"; return EDC_ERR_ARG; }
   int rc = ensure_n(ctx, n);
   if (rc) return rc;
-  size_t mbytes = n ? (size_t)msg_off[n] : 0;
-  if (n && msg_off[0] != 0) {
-    // normalise to a 0-based arena view
-    mbytes = (size_t)(msg_off[n] - msg_off[0]);
-  }
+  const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
+  if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
   rc = ensure_msg(ctx, mbytes);
   if (rc) return rc;
   if (!n) return 0;
-  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st));
-  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st));
   if (mbytes) CK(hipMemcpyAsync(ctx->msg, msg + msg_off[0], mbytes, hipMemcpyHostToDevice, ctx->st));
   if (msg_off[0] == 0) {
     CK(hipMemcpyAsync(ctx->off, msg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->st));
@@ -177,6 +171,17 @@ static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
     CK(hipMemcpyAsync(ctx->off, o.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->st));
     CK(hipStreamSynchronize(ctx->st));
   }
+  return 0;
+}
+
+// Stage the host inputs (keys, signatures, messages) into the context's device buffers.
+static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                  const uint64_t* msg_off) {
+  if (n && (!vk || !sig)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+  int rc = upload_msgs(ctx, n, msg, msg_off);
+  if (rc || !n) return rc;
+  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st));
+  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st));
   return 0;
 }
 
@@ -419,7 +424,14 @@ int edc_sign(edc_ctx* ctx, size_t n, const uint8_t* seeds, size_t nseeds, const 
              const uint8_t* msg, const uint64_t* msg_off, uint8_t* vk_out, uint8_t* sig_out) {
   if (!ctx || (n && (!seeds || !vk_out || !sig_out || !msg_off))) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  int rc = upload(ctx, n, seeds, seeds, msg, msg_off);   // stage msg + offsets
+  if (seed_index) {
+    for (size_t i = 0; i < n; ++i)
+      if (seed_index[i] >= nseeds) { ctx->err = "seed_index out of range"; return EDC_ERR_ARG; }
+  } else if (nseeds < n) {
+    ctx->err = "need one seed per item when seed_index is NULL";
+    return EDC_ERR_ARG;
+  }
+  int rc = upload_msgs(ctx, n, msg, msg_off);
   if (rc) return rc;
   if (!n) return 0;
   // aux: seeds (nseeds*32) | seed_index (n*4) | vk_out (n*32) | sig_out (n*64)

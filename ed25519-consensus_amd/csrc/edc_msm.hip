@@ -13,6 +13,7 @@
 // windows, multiplies by the cofactor and tests the identity (src/batch.rs:212-216).
 #include "edc_common.h"
 #include "edc_launch.h"
+#include "ge_quad.h"
 
 namespace edc {
 
@@ -133,57 +134,68 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
   }
 }
 
-// ---- workgroup point reductions through LDS ----
-// weighted_sum over 256 points held one per lane in lds[0..255]:
-//   returns (sum_t t * P_t, sum_t P_t) in lane 0 (valid only there).
-// 64 lanes each fold 4 consecutive points sequentially, then one wave runs a suffix scan of the
-// 64 group totals (sum_g 4g run_g = 4 sum_{g>=1} Suf_g) and two tree sums.
-__device__ void weighted_sum_256(uint32_t* lds_a, uint32_t* lds_b, int t, ge_p3& wsum, ge_p3& tot) {
-  // lds_a holds 256 ext points; lds_b scratch for 2 x 64 ext points
-  ge_p3 res, run;
-  if (t < 64) {
-    ge_p3 P3 = ld_ext(lds_a + (4 * t + 3) * EXT_WORDS);
-    ge_p3 P2 = ld_ext(lds_a + (4 * t + 2) * EXT_WORDS);
-    ge_p3 P1 = ld_ext(lds_a + (4 * t + 1) * EXT_WORDS);
-    ge_p3 P0 = ld_ext(lds_a + (4 * t + 0) * EXT_WORDS);
-    run = ge_add(P3, P2);          // P3 + P2
-    res = ge_add(run, P3);         // 2P3 + P2
-    run = ge_add(run, P1);         // P3 + P2 + P1
-    res = ge_add(res, run);        // 3P3 + 2P2 + P1
-    run = ge_add(run, P0);
-  }
+// ---- workgroup point reductions through LDS (quad-cooperative point arithmetic) ----
+// weighted_sum_256: 256 extended points lds_pts[0..255], 256 lanes = 64 quads.
+//   returns (sum_t t * P_t, sum_t P_t), valid in quad 0 (threads 0..3).
+// Quad g folds points 4g..4g+3 (res_g = P1 + 2P2 + 3P3, run_g = sum), then a Hillis-Steele
+// suffix scan of run over the 64 quads gives sum_g 4g run_g = 4 sum_{g>=1} Suf_g; two trees
+// finish. Serial depth: 5 + 6 + 2*6 + 3 quad point ops. R and S are 64-point LDS scratch.
+__device__ void weighted_sum_256(const uint32_t* lds_pts, uint32_t* R, uint32_t* S, ge_p3& wsum, ge_p3& tot) {
+  const int g = threadIdx.x >> 2;
+  const bool leader = (threadIdx.x & 3) == 0;
+  ge_p3 P3 = ld_ext(lds_pts + (4 * g + 3) * EXT_WORDS);
+  ge_p3 P2 = ld_ext(lds_pts + (4 * g + 2) * EXT_WORDS);
+  ge_p3 P1 = ld_ext(lds_pts + (4 * g + 1) * EXT_WORDS);
+  ge_p3 P0 = ld_ext(lds_pts + (4 * g + 0) * EXT_WORDS);
+  ge_p3 run = quad_add(P3, P2);
+  ge_p3 res = quad_add(run, P3);
+  run = quad_add(run, P1);
+  res = quad_add(res, run);
+  run = quad_add(run, P0);
   __syncthreads();
-  uint32_t* R = lds_b;                       // res_g
-  uint32_t* S = lds_b + 64 * EXT_WORDS;      // suffix of run_g
-  if (t < 64) { st_ext(R + t * EXT_WORDS, res); st_ext(S + t * EXT_WORDS, run); }
+  if (leader) { st_ext(R + g * EXT_WORDS, res); st_ext(S + g * EXT_WORDS, run); }
   __syncthreads();
-  // inclusive suffix scan over g (Hillis-Steele, 6 steps)
   for (int d = 1; d < 64; d <<= 1) {
+    const bool has = g + d < 64;
     ge_p3 other;
-    bool has = (t < 64) && (t + d < 64);
-    if (has) other = ld_ext(S + (t + d) * EXT_WORDS);
+    if (has) other = ld_ext(S + (g + d) * EXT_WORDS);
     __syncthreads();
-    if (has) { run = ge_add(run, other); st_ext(S + t * EXT_WORDS, run); }
+    if (has) {
+      run = quad_add(run, other);
+      if (leader) st_ext(S + g * EXT_WORDS, run);
+    }
     __syncthreads();
   }
-  // run = Suf_t. Need A = sum res_g, Bs = sum_{g>=1} Suf_g ; tot = Suf_0.
-  ge_p3 a = res, b = (t >= 1) ? run : ge_identity();
-  if (t == 0) tot = run;
+  ge_p3 a = res, b = g >= 1 ? run : ge_identity();
+  if (g == 0) tot = run;
   for (int d = 32; d >= 1; d >>= 1) {
     __syncthreads();
-    if (t < 64 && t >= d && t < 2 * d) { st_ext(R + (t - d) * EXT_WORDS + 0, a); }
+    if (leader && g >= d && g < 2 * d) { st_ext(R + (g - d) * EXT_WORDS, a); st_ext(S + (g - d) * EXT_WORDS, b); }
     __syncthreads();
-    if (t < d) a = ge_add(a, ld_ext(R + t * EXT_WORDS));
-    __syncthreads();
-    if (t < 64 && t >= d && t < 2 * d) { st_ext(S + (t - d) * EXT_WORDS, b); }
-    __syncthreads();
-    if (t < d) b = ge_add(b, ld_ext(S + t * EXT_WORDS));
+    if (g < d) {
+      a = quad_add(a, ld_ext(R + g * EXT_WORDS));
+      b = quad_add(b, ld_ext(S + g * EXT_WORDS));
+    }
   }
-  if (t == 0) {
-    // sum_t t P_t = sum_g res_g + 4 * sum_{g>=1} Suf_g
-    ge_p3 b4 = ge_dbl(ge_dbl(b));
-    wsum = ge_add(a, b4);
+  if (g == 0) wsum = quad_add(a, quad_dbl(quad_dbl(b)));
+}
+
+// plain sum of 256 extended points held one per lane (lane t has P_t); valid in quad 0.
+__device__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
+  // stage, then quad g folds 4 points, then a 64-quad tree
+  st_ext(scratch + threadIdx.x * EXT_WORDS, mine);
+  __syncthreads();
+  const int g = threadIdx.x >> 2;
+  const bool leader = (threadIdx.x & 3) == 0;
+  ge_p3 a = quad_add(quad_add(ld_ext(scratch + (4 * g) * EXT_WORDS), ld_ext(scratch + (4 * g + 1) * EXT_WORDS)),
+                     quad_add(ld_ext(scratch + (4 * g + 2) * EXT_WORDS), ld_ext(scratch + (4 * g + 3) * EXT_WORDS)));
+  for (int d = 32; d >= 1; d >>= 1) {
+    __syncthreads();
+    if (leader && g >= d && g < 2 * d) st_ext(scratch + (g - d) * EXT_WORDS, a);
+    __syncthreads();
+    if (g < d) a = quad_add(a, ld_ext(scratch + g * EXT_WORDS));
   }
+  return a;
 }
 
 constexpr int BKT_CHUNK = 4096;
@@ -254,11 +266,14 @@ __global__ void __launch_bounds__(256) k_msm_bucket(const uint32_t* __restrict__
   st_ext(lpts + t * EXT_WORDS, acc);
   __syncthreads();
   ge_p3 ws, tot;
-  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, t, ws, tot);
-  if (t == 0) {
+  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, lpts + (NSLICE + 64) * EXT_WORDS, ws, tot);
+  if (t < 4) {
     // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
-    st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_add(ws, tot));
-    st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+    ge_p3 W = quad_add(ws, tot);
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+    }
   }
 }
 
@@ -270,24 +285,17 @@ __global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__
   const int t = threadIdx.x;
   const uint32_t w = blockIdx.x;
   uint32_t* lpts = smem;
-  // plain sum of W_s: fold into a weighted sum call on T, and a separate tree over W
   st_ext(lpts + t * EXT_WORDS, ld_ext(slice_T + (size_t)(w * NSLICE + t) * EXT_WORDS));
   __syncthreads();
   ge_p3 ws, tot;
-  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, t, ws, tot);
+  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, lpts + (NSLICE + 64) * EXT_WORDS, ws, tot);
   __syncthreads();
-  // tree sum of W_s
-  ge_p3 a = ld_ext(slice_W + (size_t)(w * NSLICE + t) * EXT_WORDS);
-  for (int d = 128; d >= 1; d >>= 1) {
-    __syncthreads();
-    if (t >= d && t < 2 * d) st_ext(lpts + (t - d) * EXT_WORDS, a);
-    __syncthreads();
-    if (t < d) a = ge_add(a, ld_ext(lpts + t * EXT_WORDS));
-  }
-  if (t == 0) {
+  ge_p3 a = sum_256(ld_ext(slice_W + (size_t)(w * NSLICE + t) * EXT_WORDS), lpts);
+  if (t < 4) {
     ge_p3 x = ws;
-    for (int k = 0; k < 8; ++k) x = ge_dbl(x, k == 7);
-    st_ext(win + (size_t)w * EXT_WORDS, ge_add(a, x));
+    for (int k = 0; k < 8; ++k) x = quad_dbl(x);
+    ge_p3 r = quad_add(a, x);
+    if (t == 0) st_ext(win + (size_t)w * EXT_WORDS, r);
   }
 }
 
@@ -329,17 +337,28 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
   }
 }
 
-// Horner over windows, then x8 / identity / optional compression. Single lane by design
-// (the windows are already reduced); a later round can split the doublings across lanes.
+// Horner over windows on one quad (4 cooperating lanes), then x8 / identity / optional
+// compression (single lane; only when the caller asked for check8).
 __global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restrict__ flags,
                             int want_compress, uint8_t* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (threadIdx.x >= 4 || blockIdx.x != 0) return;
   ge_p3 acc = ld_ext(win + (size_t)(NWIN_FULL - 1) * EXT_WORDS);
   for (int w = NWIN_FULL - 2; w >= 0; --w) {
-    for (int k = 0; k < WIN_BITS; ++k) acc = ge_dbl(acc, k == WIN_BITS - 1);
-    acc = ge_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
+    for (int k = 0; k < WIN_BITS; ++k) acc = quad_dbl(acc);
+    acc = quad_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
   }
-  finish_point(acc, flags[FLAG_BAD], want_compress, out);
+  ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
+  if (threadIdx.x != 0) return;
+  ext_to_canonical_bytes(acc, out + 48);
+  const int bad = flags[FLAG_BAD];
+  reinterpret_cast<int*>(out)[0] = (!bad && ge_is_identity(c8)) ? 0 : 1;
+  reinterpret_cast<int*>(out)[1] = bad;
+  if (want_compress) {
+    uint32_t w8[8];
+    ge_compress(c8, w8);
+    for (int j = 0; j < 8; ++j)
+      for (int b = 0; b < 4; ++b) out[16 + 4 * j + b] = (uint8_t)(w8[j] >> (8 * b));
+  }
 }
 
 // combine G partial check points (canonical 128-byte records) from G shards
@@ -365,7 +384,7 @@ void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* 
                      cursor, entries, flags);
 }
 
-static const size_t kReduceLds = (size_t)(NSLICE + 128) * EXT_WORDS * sizeof(uint32_t);
+static const size_t kReduceLds = (size_t)(NSLICE + 128) * EXT_WORDS * sizeof(uint32_t);  // 256 + 2 x 64 points
 
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, const uint32_t* pts, uint32_t* slice_W, uint32_t* slice_T) {
