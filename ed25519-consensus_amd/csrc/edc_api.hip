@@ -40,6 +40,7 @@ struct edc_ctx {
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr;
   uint2* entries = nullptr;
   uint32_t *slice_W = nullptr, *slice_T = nullptr, *win = nullptr;
+  uint32_t* buckets = nullptr;  // NBIN x 256 bucket sums (extended), fixed size
   uint8_t* verdicts = nullptr;
   uint8_t* aux = nullptr;       // decode xy / sign outputs
   size_t cap_aux = 0;
@@ -65,7 +66,7 @@ static void free_workspace(edc_ctx* ctx) {
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->k, ctx->key_slot, ctx->key_index,
                   ctx->key_rep, ctx->table, ctx->slot_key, ctx->pts, ctx->scal, ctx->key_acc, ctx->u_acc,
                   ctx->counts, ctx->offsets, ctx->cursor, ctx->entries, ctx->slice_W, ctx->slice_T,
-                  ctx->win, ctx->verdicts};
+                  ctx->win, ctx->verdicts, ctx->buckets};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   ctx->vk = ctx->sig = ctx->msg = ctx->zexp = nullptr;
@@ -76,6 +77,7 @@ static void free_workspace(edc_ctx* ctx) {
   ctx->counts = ctx->offsets = ctx->cursor = nullptr;
   ctx->entries = nullptr;
   ctx->slice_W = ctx->slice_T = ctx->win = nullptr;
+  ctx->buckets = nullptr;
   ctx->verdicts = nullptr;
   ctx->cap_n = ctx->cap_T = 0;
 }
@@ -104,8 +106,8 @@ static int ensure_n(edc_ctx* ctx, size_t n) {
   CK(dalloc(&ctx->slot_key, T));
   CK(dalloc(&ctx->pts, (1 + 2 * cap) * NIELS_WORDS));
   CK(dalloc(&ctx->scal, (1 + 2 * cap) * 8));
-  CK(dalloc(&ctx->key_acc, cap * 8));
-  CK(dalloc(&ctx->u_acc, 8));
+  CK(dalloc(&ctx->key_acc, cap * KEY_ACC_LIMBS));
+  CK(dalloc(&ctx->u_acc, KEY_ACC_LIMBS));
   CK(dalloc(&ctx->counts, NBIN));
   CK(dalloc(&ctx->offsets, NBIN));
   CK(dalloc(&ctx->cursor, NBIN));
@@ -113,6 +115,7 @@ static int ensure_n(edc_ctx* ctx, size_t n) {
   CK(dalloc(&ctx->slice_W, (size_t)NBIN * EXT_WORDS));
   CK(dalloc(&ctx->slice_T, (size_t)NBIN * EXT_WORDS));
   CK(dalloc(&ctx->win, (size_t)NWIN_FULL * EXT_WORDS));
+  CK(dalloc(&ctx->buckets, msm_bucket_words()));
   CK(dalloc(&ctx->verdicts, cap));
   launch_init_basepoint(ctx->st, ctx->pts);
   CK(hipGetLastError());
@@ -200,8 +203,7 @@ static int run_batch(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t*
   hipStream_t st = ctx->st;
   CK(hipMemsetAsync(ctx->flags, 0, FLAG_COUNT * sizeof(int), st));
   CK(hipMemsetAsync(ctx->table, 0xFF, (size_t)T * sizeof(uint32_t), st));
-  CK(hipMemsetAsync(ctx->key_acc, 0, (size_t)(N ? N : 1) * 8 * sizeof(unsigned long long), st));
-  CK(hipMemsetAsync(ctx->u_acc, 0, 8 * sizeof(unsigned long long), st));
+  CK(hipMemsetAsync(ctx->u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
   CK(hipMemsetAsync(ctx->d_out, 0, 256, st));
   mark(ctx, PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, ctx->k);
@@ -209,14 +211,15 @@ static int run_batch(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t*
   launch_decompress_R(st, N, d_sig, ctx->pts, ctx->flags);
   mark(ctx, PH_KEYS);
   launch_keys(st, N, d_vk, ctx->table, T - 1, seed[0] ^ 0x5bd1e995u, ctx->slot_key, ctx->key_slot,
-              ctx->key_rep, ctx->key_index, ctx->pts, ctx->flags);
+              ctx->key_rep, ctx->key_index, ctx->pts, ctx->key_acc, ctx->flags);
   mark(ctx, PH_COEF);
   launch_coef(st, N, d_sig, ctx->k, d_z, seed, z_base, ctx->key_index, ctx->scal, ctx->key_acc, ctx->u_acc,
               ctx->flags);
   mark(ctx, PH_MSM_BIN);
   launch_msm_bin(st, N, ctx->scal, ctx->counts, ctx->offsets, ctx->cursor, ctx->entries, ctx->flags);
   mark(ctx, PH_MSM_BUCKET);
-  launch_msm_bucket(st, ctx->counts, ctx->offsets, ctx->entries, ctx->pts, ctx->slice_W, ctx->slice_T);
+  launch_msm_bucket(st, ctx->counts, ctx->offsets, ctx->entries, ctx->pts, ctx->buckets, ctx->slice_W,
+                    ctx->slice_T);
   mark(ctx, PH_MSM_TAIL);
   launch_msm_tail(st, ctx->slice_W, ctx->slice_T, ctx->win, ctx->flags, want_compress, ctx->d_out);
   mark(ctx, PH_N);

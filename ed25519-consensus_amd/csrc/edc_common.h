@@ -83,6 +83,9 @@ __device__ __forceinline__ int scalar_digit(const uint32_t s[8], int w, int& car
   return (int)raw;
 }
 
+// 64-bit limb-sum accumulators per distinct key (12 limbs of a 128 x 256-bit product)
+constexpr int KEY_ACC_LIMBS = 12;
+
 // flags slot indices
 enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_COUNT = 8 };
 

@@ -10,7 +10,7 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
 void launch_decompress_R(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
-                 uint32_t* key_index, uint32_t* pts, int* flags);
+                 uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, int* flags);
@@ -19,7 +19,9 @@ void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, const uint32_t* pts, uint32_t* slice_W, uint32_t* slice_T);
+                       const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
+                       uint32_t* slice_T);
+size_t msm_bucket_words();
 void launch_msm_tail(hipStream_t st, const uint32_t* slice_W, const uint32_t* slice_T, uint32_t* win,
                      const int* flags, int want_compress, uint8_t* out);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,

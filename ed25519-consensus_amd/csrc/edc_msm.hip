@@ -140,48 +140,52 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
 // Quad g folds points 4g..4g+3 (res_g = P1 + 2P2 + 3P3, run_g = sum), then a Hillis-Steele
 // suffix scan of run over the 64 quads gives sum_g 4g run_g = 4 sum_{g>=1} Suf_g; two trees
 // finish. Serial depth: 5 + 6 + 2*6 + 3 quad point ops. R and S are 64-point LDS scratch.
-__device__ void weighted_sum_256(const uint32_t* lds_pts, uint32_t* R, uint32_t* S, ge_p3& wsum, ge_p3& tot) {
+__device__ __forceinline__ void weighted_sum_256(const uint32_t* lds_pts, uint32_t* R, uint32_t* S, ge_p3& wsum, ge_p3& tot) {
   const int g = threadIdx.x >> 2;
   const bool leader = (threadIdx.x & 3) == 0;
-  ge_p3 P3 = ld_ext(lds_pts + (4 * g + 3) * EXT_WORDS);
-  ge_p3 P2 = ld_ext(lds_pts + (4 * g + 2) * EXT_WORDS);
-  ge_p3 P1 = ld_ext(lds_pts + (4 * g + 1) * EXT_WORDS);
-  ge_p3 P0 = ld_ext(lds_pts + (4 * g + 0) * EXT_WORDS);
-  ge_p3 run = quad_add(P3, P2);
-  ge_p3 res = quad_add(run, P3);
-  run = quad_add(run, P1);
-  res = quad_add(res, run);
-  run = quad_add(run, P0);
+  {
+    ge_p3 run = quad_add(ld_ext(lds_pts + (4 * g + 3) * EXT_WORDS), ld_ext(lds_pts + (4 * g + 2) * EXT_WORDS));
+    ge_p3 res = quad_add(run, ld_ext(lds_pts + (4 * g + 3) * EXT_WORDS));
+    run = quad_add(run, ld_ext(lds_pts + (4 * g + 1) * EXT_WORDS));
+    res = quad_add(res, run);
+    run = quad_add(run, ld_ext(lds_pts + (4 * g + 0) * EXT_WORDS));
+    __syncthreads();
+    if (leader) { st_ext(R + g * EXT_WORDS, res); st_ext(S + g * EXT_WORDS, run); }
+  }
   __syncthreads();
-  if (leader) { st_ext(R + g * EXT_WORDS, res); st_ext(S + g * EXT_WORDS, run); }
-  __syncthreads();
+  // inclusive suffix scan of run over the 64 quads: S[g] = Suf_g
   for (int d = 1; d < 64; d <<= 1) {
     const bool has = g + d < 64;
-    ge_p3 other;
-    if (has) other = ld_ext(S + (g + d) * EXT_WORDS);
+    ge_p3 mine, other;
+    if (has) { mine = ld_ext(S + g * EXT_WORDS); other = ld_ext(S + (g + d) * EXT_WORDS); }
     __syncthreads();
     if (has) {
-      run = quad_add(run, other);
-      if (leader) st_ext(S + g * EXT_WORDS, run);
+      mine = quad_add(mine, other);
+      if (leader) st_ext(S + g * EXT_WORDS, mine);
     }
     __syncthreads();
   }
-  ge_p3 a = res, b = g >= 1 ? run : ge_identity();
-  if (g == 0) tot = run;
+  if (g == 0) tot = ld_ext(S);
+  __syncthreads();
+  if (g == 0 && leader) st_ext(S, ge_identity());   // sum_{g>=1} Suf_g
+  // two trees: R (sum of res_g) and S (sum of suffixes), interleaved per step
   for (int d = 32; d >= 1; d >>= 1) {
     __syncthreads();
-    if (leader && g >= d && g < 2 * d) { st_ext(R + (g - d) * EXT_WORDS, a); st_ext(S + (g - d) * EXT_WORDS, b); }
-    __syncthreads();
     if (g < d) {
-      a = quad_add(a, ld_ext(R + g * EXT_WORDS));
-      b = quad_add(b, ld_ext(S + g * EXT_WORDS));
+      ge_p3 x = quad_add(ld_ext(R + g * EXT_WORDS), ld_ext(R + (g + d) * EXT_WORDS));
+      ge_p3 y = quad_add(ld_ext(S + g * EXT_WORDS), ld_ext(S + (g + d) * EXT_WORDS));
+      __syncthreads();
+      if (leader) { st_ext(R + g * EXT_WORDS, x); st_ext(S + g * EXT_WORDS, y); }
+    } else {
+      __syncthreads();
     }
   }
-  if (g == 0) wsum = quad_add(a, quad_dbl(quad_dbl(b)));
+  __syncthreads();
+  if (g == 0) wsum = quad_add(ld_ext(R), quad_dbl(quad_dbl(ld_ext(S))));
 }
 
 // plain sum of 256 extended points held one per lane (lane t has P_t); valid in quad 0.
-__device__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
+__device__ __forceinline__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
   // stage, then quad g folds 4 points, then a 64-quad tree
   st_ext(scratch + threadIdx.x * EXT_WORDS, mine);
   __syncthreads();
@@ -200,31 +204,23 @@ __device__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
 
 constexpr int BKT_CHUNK = 4096;
 
-// one workgroup per bin (window w, slice s): bucket sums S_b for b = 256 s + t + 1 and
-// W_s = sum_t (t+1) S_t, T_s = sum_t S_t
-__global__ void __launch_bounds__(256) k_msm_bucket(const uint32_t* __restrict__ counts,
-                                                    const uint32_t* __restrict__ offsets,
-                                                    const uint2* __restrict__ entries,
-                                                    const uint32_t* __restrict__ pts,
-                                                    uint32_t* __restrict__ slice_W,
-                                                    uint32_t* __restrict__ slice_T) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* lidx = smem;                               // BKT_CHUNK
-  uint32_t* lcnt = smem + BKT_CHUNK;                   // 256
-  uint32_t* lstart = lcnt + NSLICE;                    // 256
-  uint32_t* lcur = lstart + NSLICE;                    // 256
-  uint32_t* lpts = smem;                               // reused: 256 ext + 128 ext (after accumulation)
+// one workgroup per bin (window w, slice s), one lane per bucket: S_b for b = 256 s + t + 1.
+// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK), then lane t walks its
+// bucket's entries with the next Niels point prefetched under the current 7M mixed addition.
+__global__ void __launch_bounds__(256) k_msm_accum(const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const uint2* __restrict__ entries,
+                                                   const uint32_t* __restrict__ pts,
+                                                   uint32_t* __restrict__ buckets) {
+  __shared__ uint32_t lidx[BKT_CHUNK];
+  __shared__ uint32_t lcnt[NSLICE];
+  __shared__ uint32_t lstart[NSLICE];
+  __shared__ uint32_t lcur[NSLICE];
   const int t = threadIdx.x;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
+  if (E == 0) return;
   const uint32_t off = offsets[bin];
-  if (E == 0) {
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
-    }
-    return;
-  }
   ge_p3 acc = ge_identity();
   for (uint32_t c0 = 0; c0 < E; c0 += BKT_CHUNK) {
     const uint32_t ch = min((uint32_t)BKT_CHUNK, E - c0);
@@ -233,7 +229,6 @@ __global__ void __launch_bounds__(256) k_msm_bucket(const uint32_t* __restrict__
     for (uint32_t e = t; e < ch; e += 256) atomicAdd(&lcnt[entries[off + c0 + e].y], 1u);
     __syncthreads();
     if (t < 64) {
-      // exclusive scan of 256 counts by one wave (4 per lane)
       uint32_t c[4], s = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) { c[j] = lcnt[4 * t + j]; s += c[j]; }
@@ -255,21 +250,45 @@ __global__ void __launch_bounds__(256) k_msm_bucket(const uint32_t* __restrict__
     }
     __syncthreads();
     const uint32_t beg = lstart[t], cnt = lcnt[t];
-    for (uint32_t j = 0; j < cnt; ++j) {
-      uint32_t e = lidx[beg + j];
+    if (cnt) {
+      uint32_t e = lidx[beg];
       ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-      if (e >> 31) q = ge_niels_neg(q);
-      acc = ge_madd(acc, q);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t e_next = (j + 1 < cnt) ? lidx[beg + j + 1] : e;
+        ge_niels q_next = ld_niels(pts, e_next & 0x7FFFFFFFu);
+        if (e >> 31) q = ge_niels_neg(q);
+        acc = ge_madd(acc, q);
+        e = e_next;
+        q = q_next;
+      }
     }
     __syncthreads();
   }
-  st_ext(lpts + t * EXT_WORDS, acc);
+  st_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS, acc);
+}
+
+// one workgroup per bin: W_s = sum_t (t+1) S_t and T_s = sum_t S_t (quad-cooperative)
+__global__ void __launch_bounds__(256) k_msm_reduce(const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ buckets,
+                                                    uint32_t* __restrict__ slice_W,
+                                                    uint32_t* __restrict__ slice_T) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int t = threadIdx.x;
+  const uint32_t bin = blockIdx.x;
+  if (counts[bin] == 0) {
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
+    }
+    return;
+  }
+  uint32_t* lpts = smem;
+  st_ext(lpts + t * EXT_WORDS, ld_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS));
   __syncthreads();
   ge_p3 ws, tot;
   weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, lpts + (NSLICE + 64) * EXT_WORDS, ws, tot);
   if (t < 4) {
-    // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
-    ge_p3 W = quad_add(ws, tot);
+    ge_p3 W = quad_add(ws, tot);       // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
     if (t == 0) {
       st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
       st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
@@ -299,26 +318,37 @@ __global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__
   }
 }
 
-__device__ __forceinline__ void ext_to_canonical_bytes(const ge_p3& P, uint8_t* out) {
+__device__ __forceinline__ void fe_to_bytes32(const fe& a, uint8_t* out) {
   uint32_t w[8];
-  const fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
-  for (int k = 0; k < 4; ++k) {
-    fe_to_words(*c[k], w);
-    for (int j = 0; j < 8; ++j)
-      for (int b = 0; b < 4; ++b) out[32 * k + 4 * j + b] = (uint8_t)(w[j] >> (8 * b));
-  }
+  fe_to_words(a, w);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) out[4 * j + b] = (uint8_t)(w[j] >> (8 * b));
+}
+
+__device__ __forceinline__ void ext_to_canonical_bytes(const ge_p3& P, uint8_t* out) {
+  fe_to_bytes32(P.X, out);
+  fe_to_bytes32(P.Y, out + 32);
+  fe_to_bytes32(P.Z, out + 64);
+  fe_to_bytes32(P.T, out + 96);
+}
+
+__device__ __forceinline__ fe fe_from_bytes32(const uint8_t* in) {
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    w[j] = (uint32_t)in[4 * j] | ((uint32_t)in[4 * j + 1] << 8) | ((uint32_t)in[4 * j + 2] << 16) |
+           ((uint32_t)in[4 * j + 3] << 24);
+  return fe_from_words(w);
 }
 
 __device__ __forceinline__ ge_p3 ext_from_canonical_bytes(const uint8_t* in) {
   ge_p3 P;
-  fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
-  for (int k = 0; k < 4; ++k) {
-    uint32_t w[8];
-    for (int j = 0; j < 8; ++j)
-      w[j] = (uint32_t)in[32 * k + 4 * j] | ((uint32_t)in[32 * k + 4 * j + 1] << 8) |
-             ((uint32_t)in[32 * k + 4 * j + 2] << 16) | ((uint32_t)in[32 * k + 4 * j + 3] << 24);
-    *c[k] = fe_from_words(w);
-  }
+  P.X = fe_from_bytes32(in);
+  P.Y = fe_from_bytes32(in + 32);
+  P.Z = fe_from_bytes32(in + 64);
+  P.T = fe_from_bytes32(in + 96);
   return P;
 }
 
@@ -387,10 +417,13 @@ void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* 
 static const size_t kReduceLds = (size_t)(NSLICE + 128) * EXT_WORDS * sizeof(uint32_t);  // 256 + 2 x 64 points
 
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, const uint32_t* pts, uint32_t* slice_W, uint32_t* slice_T) {
-  hipLaunchKernelGGL(k_msm_bucket, dim3(NBIN), dim3(256), kReduceLds, st, counts, offsets, entries, pts,
-                     slice_W, slice_T);
+                       const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
+                       uint32_t* slice_T) {
+  hipLaunchKernelGGL(k_msm_accum, dim3(NBIN), dim3(256), 0, st, counts, offsets, entries, pts, buckets);
+  hipLaunchKernelGGL(k_msm_reduce, dim3(NBIN), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
 }
+
+size_t msm_bucket_words() { return (size_t)NBIN * NSLICE * EXT_WORDS; }
 
 void launch_msm_tail(hipStream_t st, const uint32_t* slice_W, const uint32_t* slice_T, uint32_t* win,
                      const int* flags, int want_compress, uint8_t* out) {

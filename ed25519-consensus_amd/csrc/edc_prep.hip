@@ -23,11 +23,12 @@ __global__ void __launch_bounds__(256) k_challenge(uint32_t n, const uint8_t* __
   if (i >= n) return;
   uint64_t o0 = off[i], o1 = off[i + 1];
   sha_src s{sig + (size_t)i * 64, vk + (size_t)i * 32, msg + o0, o1 - o0};
-  uint8_t d[64];
-  sha512_src(s, d);
-  sc k = sc_from_digest(d);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) k_out[(size_t)i * 8 + j] = k.v[j];
+  uint32_t x[16];
+  sha512_src_le_words(s, x);
+  sc k = sc_reduce_wide(x);
+  uint4* kp = reinterpret_cast<uint4*>(k_out + (size_t)i * 8);
+  kp[0] = make_uint4(k.v[0], k.v[1], k.v[2], k.v[3]);
+  kp[1] = make_uint4(k.v[4], k.v[5], k.v[6], k.v[7]);
 }
 
 // R_i -> points[1 + i]
@@ -65,6 +66,7 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
                                                     uint32_t salt, uint32_t* __restrict__ slot_key,
                                                     uint32_t* __restrict__ key_slot_of_sig,
                                                     uint32_t* __restrict__ key_rep,
+                                                    unsigned long long* __restrict__ key_acc,
                                                     int* __restrict__ flags) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -80,6 +82,8 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
         slot_key[h] = kidx;
         key_rep[kidx] = i;
         key_slot_of_sig[i] = h;
+#pragma unroll
+        for (int j = 0; j < KEY_ACC_LIMBS; ++j) key_acc[(size_t)kidx * KEY_ACC_LIMBS + j] = 0;
         return;
       }
       cur = prev;
@@ -121,24 +125,36 @@ __global__ void __launch_bounds__(256) k_decompress_A(uint32_t n, const uint8_t*
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
 
-// z_i as 4 LE words of the ChaCha20 keystream at global index zi
-__device__ __forceinline__ void draw_z(const uint32_t seed[8], uint64_t zi, uint32_t z[4]) {
-  uint32_t blk[16];
-  chacha20_block(seed, zi >> 2, blk);
-  int q = (int)(zi & 3);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) z[j] = blk[4 * q + j];
-}
-
 struct seed8 { uint32_t w[8]; };
 
-constexpr int COEF_CHUNK = 2048;   // signatures per workgroup
-constexpr int COEF_SLOTS = 256;    // LDS key-accumulator slots
+constexpr int COEF_SIGS_PER_THREAD = 8;             // two ChaCha blocks -> z for 8 signatures
+constexpr int COEF_CHUNK = 256 * COEF_SIGS_PER_THREAD;
+constexpr int COEF_SLOTS = 256;                     // LDS key-accumulator slots
+constexpr int PL = 12;                              // limbs of a 128 x 256-bit product
+
+// r[0..11] = z (4 limbs) * s (8 limbs), exact
+__device__ __forceinline__ void mul_128x256(const uint32_t z[4], const uint32_t s[8], uint32_t r[PL]) {
+#pragma unroll
+  for (int i = 0; i < PL; ++i) r[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint64_t t = (uint64_t)z[i] * s[j] + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    r[i + 8] = (uint32_t)c;
+  }
+}
 
 // Coefficients of the batch equation (reference src/batch.rs:193-198):
 //   B_coeff -= z*s ; A_coeff[key] += z*k ; R coefficient = z.
-// Integer limb sums are order-independent, so the LDS pre-aggregation + 64-bit atomics give
-// bit-identical coefficients for any schedule.
+// The 381-bit products are NOT reduced per signature: their 32-bit limbs are summed exactly in
+// 64-bit accumulators (per thread in registers for sum z*s, per key through LDS slots / global
+// 64-bit atomics for sum z*k) and reduced mod l once (k_key_final). Integer sums are
+// order-independent, so any schedule gives bit-identical coefficients.
 __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restrict__ sig,
                                               const uint32_t* __restrict__ kscal,
                                               const uint8_t* __restrict__ zexp, seed8 seed,
@@ -148,73 +164,105 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               unsigned long long* __restrict__ u_acc,
                                               int* __restrict__ flags) {
   __shared__ uint32_t tag[COEF_SLOTS];
-  __shared__ unsigned long long acc[COEF_SLOTS][8];
-  __shared__ unsigned long long uacc[8];
+  __shared__ unsigned long long acc[COEF_SLOTS][PL];
+  __shared__ unsigned long long red[4][PL];
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
     tag[s] = 0xFFFFFFFFu;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[s][j] = 0;
+    for (int j = 0; j < PL; ++j) acc[s][j] = 0;
   }
-  if (threadIdx.x < 8) uacc[threadIdx.x] = 0;
   __syncthreads();
+  unsigned long long ua[PL];
+#pragma unroll
+  for (int j = 0; j < PL; ++j) ua[j] = 0;
   bool bad = false;
-  uint32_t base = blockIdx.x * COEF_CHUNK;
-  for (uint32_t t = threadIdx.x; t < COEF_CHUNK; t += blockDim.x) {
-    uint32_t i = base + t;
-    if (i >= n) break;
-    uint32_t z[4];
-    if (zexp) {
-      const uint32_t* zp = reinterpret_cast<const uint32_t*>(zexp + (size_t)i * 16);
+  const uint32_t base = blockIdx.x * COEF_CHUNK;
+  for (int grp = 0; grp < COEF_SIGS_PER_THREAD / 4; ++grp) {
+    const uint32_t i0 = base + 4 * (threadIdx.x + 256 * grp);
+    if (i0 >= n) break;
+    uint32_t blk[16];
+    const bool aligned = ((zbase + i0) & 3) == 0;
+    if (!zexp && aligned) chacha20_block(seed.w, (zbase + i0) >> 2, blk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) z[j] = zp[j];
-    } else {
-      draw_z(seed.w, zbase + i, z);
-    }
-    uint32_t sw[8];
-    ld_words8(sig + (size_t)i * 64 + 32, sw);
-    bad |= !sc_is_canonical(sw);
-    sc s, k;
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t i = i0 + q;
+      if (i >= n) break;
+      uint32_t z[4];
+      if (zexp) {
+        const uint4 zz = *reinterpret_cast<const uint4*>(zexp + (size_t)i * 16);
+        z[0] = zz.x; z[1] = zz.y; z[2] = zz.z; z[3] = zz.w;
+      } else if (aligned) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { s.v[j] = sw[j]; k.v[j] = kscal[(size_t)i * 8 + j]; }
-    sc u = sc_mul128(z, s);
-    sc v = sc_mul128(z, k);
-    // R coefficient = z (point 1 + i)
-    uint32_t* sp = scal + (size_t)(1 + i) * 8;
+        for (int j = 0; j < 4; ++j) z[j] = blk[4 * q + j];
+      } else {
+        uint32_t b2[16];
+        chacha20_block(seed.w, (zbase + i) >> 2, b2);
+        const int o = (int)((zbase + i) & 3);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sp[j] = j < 4 ? z[j] : 0u;
+        for (int j = 0; j < 4; ++j) z[j] = b2[4 * o + j];
+      }
+      uint32_t sw[8], kw[8];
+      ld_words8(sig + (size_t)i * 64 + 32, sw);
+      const uint4* kp = reinterpret_cast<const uint4*>(kscal + (size_t)i * 8);
+      uint4 k0 = kp[0], k1 = kp[1];
+      kw[0] = k0.x; kw[1] = k0.y; kw[2] = k0.z; kw[3] = k0.w; kw[4] = k1.x; kw[5] = k1.y; kw[6] = k1.z; kw[7] = k1.w;
+      bad |= !sc_is_canonical(sw);
+      uint32_t u[PL], v[PL];
+      mul_128x256(z, sw, u);
+      mul_128x256(z, kw, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&uacc[j], (unsigned long long)u.v[j]);
-    uint32_t key = key_index[i];
-    uint32_t slot = key & (COEF_SLOTS - 1);
-    uint32_t prev = atomicCAS(&tag[slot], 0xFFFFFFFFu, key);
-    if (prev == 0xFFFFFFFFu || prev == key) {
+      for (int j = 0; j < PL; ++j) ua[j] += u[j];
+      uint4* sp = reinterpret_cast<uint4*>(scal + (size_t)(1 + i) * 8);
+      sp[0] = make_uint4(z[0], z[1], z[2], z[3]);
+      sp[1] = make_uint4(0, 0, 0, 0);
+      const uint32_t key = key_index[i];
+      const uint32_t slot = key & (COEF_SLOTS - 1);
+      const uint32_t prev = atomicCAS(&tag[slot], 0xFFFFFFFFu, key);
+      if (prev == 0xFFFFFFFFu || prev == key) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&acc[slot][j], (unsigned long long)v.v[j]);
-    } else {
+        for (int j = 0; j < PL; ++j) atomicAdd(&acc[slot][j], (unsigned long long)v[j]);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&key_acc[(size_t)key * 8 + j], (unsigned long long)v.v[j]);
+        for (int j = 0; j < PL; ++j) atomicAdd(&key_acc[(size_t)key * PL + j], (unsigned long long)v[j]);
+      }
     }
   }
   if (bad) atomicOr(&flags[FLAG_BAD], 1);
+  // workgroup reduction of the per-thread z*s limb sums (64-bit shuffles, then LDS)
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    unsigned long long x = ua[j];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_down(x, d, 64);
+    ua[j] = x;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) red[wv][j] = ua[j];
+  }
   __syncthreads();
+  if (threadIdx.x < PL) {
+    unsigned long long x = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&u_acc[threadIdx.x], x);
+  }
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
-    uint32_t key = tag[s];
+    const uint32_t key = tag[s];
     if (key != 0xFFFFFFFFu) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(&key_acc[(size_t)key * 8 + j], acc[s][j]);
+      for (int j = 0; j < PL; ++j) atomicAdd(&key_acc[(size_t)key * PL + j], acc[s][j]);
     }
   }
-  if (threadIdx.x < 8) atomicAdd(&u_acc[threadIdx.x], uacc[threadIdx.x]);
 }
 
-// sum_j L[j] * 2^(32 j) mod l, L[j] < 2^64
+// sum_j L[j] * 2^(32 j) mod l for PL limb sums L[j] < 2^64 (value < 2^448)
 __device__ __forceinline__ sc reduce_limb_sums(const unsigned long long* L) {
   uint32_t x[16];
   unsigned long long carry = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    unsigned long long lo = j < 8 ? (L[j] & 0xFFFFFFFFull) : 0ull;
-    unsigned long long hi = (j >= 1 && j <= 8) ? (L[j - 1] >> 32) : 0ull;
+    unsigned long long lo = j < PL ? (L[j] & 0xFFFFFFFFull) : 0ull;
+    unsigned long long hi = (j >= 1 && j <= PL) ? (L[j - 1] >> 32) : 0ull;
     unsigned long long t = lo + hi + carry;
     x[j] = (uint32_t)t;
     carry = t >> 32;
@@ -229,7 +277,7 @@ __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned lo
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   if (j < m) {
-    sc a = reduce_limb_sums(key_acc + (size_t)j * 8);
+    sc a = reduce_limb_sums(key_acc + (size_t)j * PL);
 #pragma unroll
     for (int q = 0; q < 8; ++q) scal[(size_t)(1 + n + j) * 8 + q] = a.v[q];
   }
@@ -257,10 +305,10 @@ void launch_decompress_R(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
-                 uint32_t* key_index, uint32_t* pts, int* flags) {
+                 uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags) {
   if (!n) return;
   hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt,
-                     slot_key, key_slot_of_sig, key_rep, flags);
+                     slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index);
   hipLaunchKernelGGL(k_decompress_A, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags);

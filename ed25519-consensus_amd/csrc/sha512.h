@@ -9,13 +9,12 @@
 
 namespace edc {
 
+// round constants: __constant__ on the device (wave-uniform scalar loads), const on the host
 #if defined(__HIP_DEVICE_COMPILE__)
-#define EDC_CONST __constant__
+__constant__ uint64_t SHA512_K[80] = {
 #else
-#define EDC_CONST static const
+static const uint64_t SHA512_K[80] = {
 #endif
-
-EDC_CONST uint64_t SHA512_K[80] = {
     0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
     0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
     0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
@@ -37,32 +36,94 @@ EDC_CONST uint64_t SHA512_K[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
-EDC_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit words viewed as 32-bit halves through bit casts (free register-pair views): rotates are
+// two v_alignbit_b32, three-way xors one v_bitop3_b32 per half, adds v_lshl_add_u64.
+struct w64 { uint32_t lo, hi; };
 
-EDC_HD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
-  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-  for (int t = 0; t < 80; ++t) {
-    uint64_t wt;
-    if (t < 16) {
-      wt = w[t];
-    } else {
-      uint64_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
-      uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
-      w[t & 15] = wt;
-    }
-    uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-    uint64_t ch = (e & f) ^ (~e & g);
-    uint64_t t1 = hh + S1 + ch + SHA512_K[t] + wt;
-    uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-    uint64_t maj = (a & b) ^ (a & c) ^ (b & c);
-    uint64_t t2 = S0 + maj;
-    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-  }
-  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+EDC_HD w64 mk64(uint64_t x) { return w64{(uint32_t)x, (uint32_t)(x >> 32)}; }
+EDC_HD uint64_t un64(w64 x) { return ((uint64_t)x.hi << 32) | x.lo; }
+
+// funnel shift right of hi:lo by n (0 < n < 32)
+EDC_HD uint32_t fshr32(uint32_t hi, uint32_t lo, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> n);
+#endif
 }
+EDC_HD uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+EDC_HD w64 rotr(w64 x, int n) {
+  if (n < 32) return w64{fshr32(x.hi, x.lo, n), fshr32(x.lo, x.hi, n)};
+  return w64{fshr32(x.lo, x.hi, n - 32), fshr32(x.hi, x.lo, n - 32)};
+}
+EDC_HD w64 shr(w64 x, int n) { return w64{fshr32(x.hi, x.lo, n), x.hi >> n}; }
+EDC_HD w64 xor3(w64 a, w64 b, w64 c) { return w64{xor3_32(a.lo, b.lo, c.lo), xor3_32(a.hi, b.hi, c.hi)}; }
+EDC_HD w64 add(w64 a, w64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  unsigned int carry;
+  uint32_t lo = __builtin_addc(a.lo, b.lo, 0u, &carry);
+  unsigned int c2;
+  uint32_t hi = __builtin_addc(a.hi, b.hi, carry, &c2);
+  return w64{lo, hi};
+#else
+  return mk64(un64(a) + un64(b));
+#endif
+}
+EDC_HD w64 ch(w64 e, w64 f, w64 g) { return w64{(e.lo & f.lo) ^ (~e.lo & g.lo), (e.hi & f.hi) ^ (~e.hi & g.hi)}; }
+EDC_HD w64 maj(w64 a, w64 b, w64 c) {
+  return w64{(a.lo & b.lo) ^ (a.lo & c.lo) ^ (b.lo & c.lo), (a.hi & b.hi) ^ (a.hi & c.hi) ^ (b.hi & c.hi)};
+}
+
+#define EDC_SHA_ROUND(a, b, c, d, e, f, g, h, k, wt)                                              \
+  {                                                                                              \
+    w64 t1 = add(add(add(h, xor3(rotr(e, 14), rotr(e, 18), rotr(e, 41))), add(ch(e, f, g), k)), wt); \
+    w64 t2 = add(xor3(rotr(a, 28), rotr(a, 34), rotr(a, 39)), maj(a, b, c));                         \
+    d = add(d, t1);                                                                              \
+    h = add(t1, t2);                                                                             \
+  }
+
+// 80 rounds as 5 x 16: the 16-round body is unrolled (message words in registers, the eight
+// working variables renamed instead of moved), the 5 passes are a loop.
+EDC_HD void sha512_compress(uint64_t hs[8], const uint64_t win[16]) {
+  w64 w[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) w[t] = mk64(win[t]);
+  w64 a = mk64(hs[0]), b = mk64(hs[1]), c = mk64(hs[2]), d = mk64(hs[3]);
+  w64 e = mk64(hs[4]), f = mk64(hs[5]), g = mk64(hs[6]), h = mk64(hs[7]);
+#pragma unroll 1
+  for (int r = 0; r < 5; ++r) {
+    if (r) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        w64 w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        w64 s0 = xor3(rotr(w15, 1), rotr(w15, 8), shr(w15, 7));
+        w64 s1 = xor3(rotr(w2, 19), rotr(w2, 61), shr(w2, 6));
+        w[j] = add(add(w[j], s0), add(w[(j + 9) & 15], s1));
+      }
+    }
+    const uint64_t* K = SHA512_K + 16 * r;
+#pragma unroll
+    for (int j = 0; j < 16; j += 8) {
+      EDC_SHA_ROUND(a, b, c, d, e, f, g, h, mk64(K[j + 0]), w[j + 0]);
+      EDC_SHA_ROUND(h, a, b, c, d, e, f, g, mk64(K[j + 1]), w[j + 1]);
+      EDC_SHA_ROUND(g, h, a, b, c, d, e, f, mk64(K[j + 2]), w[j + 2]);
+      EDC_SHA_ROUND(f, g, h, a, b, c, d, e, mk64(K[j + 3]), w[j + 3]);
+      EDC_SHA_ROUND(e, f, g, h, a, b, c, d, mk64(K[j + 4]), w[j + 4]);
+      EDC_SHA_ROUND(d, e, f, g, h, a, b, c, mk64(K[j + 5]), w[j + 5]);
+      EDC_SHA_ROUND(c, d, e, f, g, h, a, b, mk64(K[j + 6]), w[j + 6]);
+      EDC_SHA_ROUND(b, c, d, e, f, g, h, a, mk64(K[j + 7]), w[j + 7]);
+    }
+  }
+  hs[0] += un64(a); hs[1] += un64(b); hs[2] += un64(c); hs[3] += un64(d);
+  hs[4] += un64(e); hs[5] += un64(f); hs[6] += un64(g); hs[7] += un64(h);
+}
+#undef EDC_SHA_ROUND
 
 EDC_HD void sha512_init(uint64_t h[8]) {
   h[0] = 0x6a09e667f3bcc908ull; h[1] = 0xbb67ae8584caa73bull; h[2] = 0x3c6ef372fe94f82bull;
@@ -79,16 +140,37 @@ struct sha_src {
   uint64_t mlen;
 };
 
-EDC_HD uint64_t load_be64(const uint8_t* p) {
-  uint64_t w = 0;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) w = (w << 8) | p[b];
-  return w;
+EDC_HD uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
 }
 
+// big-endian 64-bit word from an 8-byte-aligned pointer (R / A / seed heads)
+EDC_HD uint64_t load_be64(const uint8_t* p) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+  return ((uint64_t)bswap32(q[0]) << 32) | bswap32(q[1]);
+}
+
+// 4-byte-aligned dword containing byte p. Reading it never leaves the page of p, so it is safe
+// for any p inside the message arena.
+EDC_HD uint32_t ld_dword_at(uintptr_t a) { return *reinterpret_cast<const uint32_t*>(a); }
+
 // Big-endian word of the padded message tail starting at message byte j (j may exceed mlen).
+// Full words are assembled from aligned dwords (funnel shifts, v_alignbyte on gfx950); only the
+// last partial word of a message takes the byte path.
 EDC_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t j) {
-  if (j + 8 <= mlen) return load_be64(m + j);
+  if (j + 8 <= mlen) {
+    const uintptr_t p = (uintptr_t)(m + j);
+    const uintptr_t a = p & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint32_t d0 = ld_dword_at(a), d1 = ld_dword_at(a + 4);
+    uint32_t lo = d0, hi = d1;
+    if (sh) {
+      const uint32_t d2 = ld_dword_at(a + 8);
+      lo = (d0 >> sh) | (d1 << (32 - sh));
+      hi = (d1 >> sh) | (d2 << (32 - sh));
+    }
+    return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
+  }
   uint64_t w = 0;
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
@@ -99,13 +181,13 @@ EDC_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t j) {
   return w;
 }
 
-// SHA-512(head0[0..32) || head1[0..32) || msg[0..mlen)); digest bytes in out[0..64).
-EDC_HD void sha512_src(const sha_src& s, uint8_t out[64]) {
-  uint64_t h[8];
+// SHA-512(head0[0..32) || head1[0..32) || msg[0..mlen)) as the 8 big-endian state words.
+EDC_HD void sha512_src_state(const sha_src& s, uint64_t h[8]) {
   sha512_init(h);
   const uint64_t hlen = s.head1 ? 64 : 32;
   const uint64_t total = hlen + s.mlen;
   const uint64_t nblocks = (total + 17 + 127) / 128;
+#pragma unroll 1
   for (uint64_t blk = 0; blk < nblocks; ++blk) {
     uint64_t w[16];
 #pragma unroll
@@ -121,10 +203,27 @@ EDC_HD void sha512_src(const sha_src& s, uint8_t out[64]) {
     }
     sha512_compress(h, w);
   }
+}
+
+// digest bytes in out[0..64)
+EDC_HD void sha512_src(const sha_src& s, uint8_t out[64]) {
+  uint64_t h[8];
+  sha512_src_state(s, h);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int b = 0; b < 8; ++b) out[8 * i + b] = (uint8_t)(h[i] >> (56 - 8 * b));
+}
+
+// digest as 16 little-endian 32-bit words (the 512-bit LE integer Scalar::from_hash reduces)
+EDC_HD void sha512_src_le_words(const sha_src& s, uint32_t x[16]) {
+  uint64_t h[8];
+  sha512_src_state(s, h);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    x[2 * i] = bswap32((uint32_t)(h[i] >> 32));
+    x[2 * i + 1] = bswap32((uint32_t)h[i]);
+  }
 }
 
 }  // namespace edc
