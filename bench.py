@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
+    ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (submit/wait pipelining)")
     args = ap.parse_args()
 
     import torch
@@ -128,6 +129,33 @@ def main():
     lib = eng.lib
     check8 = ctypes.create_string_buffer(32)
 
+    pending = []
+
+    def submit():
+        t = lib.edc_batch_submit_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
+                                        zseed, 0, None, 0)
+        if t < 0:
+            eng._check(t)
+        pending.append(t)
+
+    def wait_oldest():
+        rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
+        return eng._check(rc)
+
+    def run_steps(k):
+        """k full batch verifications; with --inflight 2 batch i+1 is enqueued before batch i's
+        verdict is collected (the verdict of every batch is still waited for inside the loop)."""
+        if world > 1 or args.inflight <= 1:
+            return [step() for _ in range(k)]
+        codes = []
+        for _ in range(k):
+            if len(pending) >= args.inflight:
+                codes.append(wait_oldest())
+            submit()
+        while pending:
+            codes.append(wait_oldest())
+        return codes
+
     def step():
         if world == 1:
             # Verifier::verify returns only Ok/Err: no [8]*check compression in the timed loop
@@ -146,13 +174,12 @@ def main():
                                          sharded.torch_allgather_fn(dist, dev), rank, world, base)
         return code
 
-    for _ in range(args.warmup):
-        code = step()
+    run_steps(args.warmup)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    codes = [step() for _ in range(args.steps)]
+    codes = run_steps(args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -213,6 +240,7 @@ def main():
             "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
             "config": {"workload": "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs",
                        "sigs_per_gpu": n, "validators": args.keys, "msg_len": args.msg_len,
+                       "inflight": args.inflight if world == 1 else 1,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress_R",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

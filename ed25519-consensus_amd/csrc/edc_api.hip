@@ -22,17 +22,14 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, count * sizeof(T));
 }
 
+constexpr int kSlots = 2;  // batches that can be in flight per context
+
 }  // namespace
 
-struct edc_ctx {
-  int device = 0;
+// One in-flight batch: its own HIP stream and every per-batch device buffer.
+struct Slot {
   hipStream_t st = nullptr;
-  std::string err;
-  uint32_t* btab = nullptr;   // [1..8]B affine Niels
-  // grow-only workspace
-  size_t cap_n = 0, cap_msg = 0, cap_T = 0;
-  uint8_t *vk = nullptr, *sig = nullptr, *msg = nullptr, *zexp = nullptr;
-  uint64_t* off = nullptr;
+  size_t cap_n = 0, cap_T = 0;
   uint32_t *k = nullptr, *key_slot = nullptr, *key_index = nullptr, *key_rep = nullptr;
   uint32_t *table = nullptr, *slot_key = nullptr;
   uint32_t *pts = nullptr, *scal = nullptr;
@@ -41,16 +38,32 @@ struct edc_ctx {
   uint2* entries = nullptr;
   uint32_t *slice_W = nullptr, *slice_T = nullptr, *win = nullptr;
   uint32_t* buckets = nullptr;  // NBIN x 256 bucket sums (extended), fixed size
-  uint8_t* verdicts = nullptr;
-  uint8_t* aux = nullptr;       // decode xy / sign outputs
-  size_t cap_aux = 0;
   int* flags = nullptr;
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
-  bool timing = false;
   hipEvent_t ev[PH_N + 1] = {};
+  bool pending = false;         // submitted, not yet waited
+  bool timed = false;
+  int64_t ticket = -1;
+};
+
+struct edc_ctx {
+  int device = 0;
+  std::string err;
+  uint32_t* btab = nullptr;     // [1..8]B affine Niels
+  Slot slot[kSlots];
+  // staging for the host-pointer entry points (used on slot 0's stream)
+  size_t cap_n = 0, cap_msg = 0, cap_aux = 0;
+  uint8_t *vk = nullptr, *sig = nullptr, *msg = nullptr, *zexp = nullptr;
+  uint64_t* off = nullptr;
+  uint32_t* kbuf = nullptr;
+  uint8_t* verdicts = nullptr;
+  uint8_t* aux = nullptr;       // decode xy / sign outputs / partials
+  bool timing = false;
   float last_ms[PH_N] = {};
   int nlast = 0;
+  int64_t next_ticket = 0;
+  hipStream_t st() const { return slot[0].st; }
 };
 
 #define CK(expr)                                                        \
@@ -62,24 +75,17 @@ struct edc_ctx {
     }                                                                   \
   } while (0)
 
-static void free_workspace(edc_ctx* ctx) {
-  void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->k, ctx->key_slot, ctx->key_index,
-                  ctx->key_rep, ctx->table, ctx->slot_key, ctx->pts, ctx->scal, ctx->key_acc, ctx->u_acc,
-                  ctx->counts, ctx->offsets, ctx->cursor, ctx->entries, ctx->slice_W, ctx->slice_T,
-                  ctx->win, ctx->verdicts, ctx->buckets};
+static void free_slot_buffers(Slot& s) {
+  void* ptrs[] = {s.k, s.key_slot, s.key_index, s.key_rep, s.table, s.slot_key, s.pts, s.scal, s.key_acc,
+                  s.u_acc, s.counts, s.offsets, s.cursor, s.entries, s.slice_W, s.slice_T, s.win, s.buckets};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  ctx->vk = ctx->sig = ctx->msg = ctx->zexp = nullptr;
-  ctx->off = nullptr;
-  ctx->k = ctx->key_slot = ctx->key_index = ctx->key_rep = ctx->table = ctx->slot_key = nullptr;
-  ctx->pts = ctx->scal = nullptr;
-  ctx->key_acc = ctx->u_acc = nullptr;
-  ctx->counts = ctx->offsets = ctx->cursor = nullptr;
-  ctx->entries = nullptr;
-  ctx->slice_W = ctx->slice_T = ctx->win = nullptr;
-  ctx->buckets = nullptr;
-  ctx->verdicts = nullptr;
-  ctx->cap_n = ctx->cap_T = 0;
+  s.k = s.key_slot = s.key_index = s.key_rep = s.table = s.slot_key = s.pts = s.scal = nullptr;
+  s.key_acc = s.u_acc = nullptr;
+  s.counts = s.offsets = s.cursor = nullptr;
+  s.entries = nullptr;
+  s.slice_W = s.slice_T = s.win = s.buckets = nullptr;
+  s.cap_n = s.cap_T = 0;
 }
 
 static size_t next_pow2(size_t x) {
@@ -88,45 +94,70 @@ static size_t next_pow2(size_t x) {
   return p;
 }
 
+static int init_slot(edc_ctx* ctx, Slot& s) {
+  if (s.st) return 0;
+  CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+  CK(dalloc(&s.flags, FLAG_COUNT));
+  CK(dalloc(&s.d_out, 256));
+  CK(hipHostMalloc((void**)&s.h_out, 256));
+  for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
+  return 0;
+}
+
+static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
+  int rc = init_slot(ctx, s);
+  if (rc) return rc;
+  if (n <= s.cap_n && s.pts) return 0;
+  CK(hipStreamSynchronize(s.st));
+  free_slot_buffers(s);
+  const size_t cap = n < 1024 ? 1024 : n + n / 8;
+  const size_t T = next_pow2(2 * cap);
+  CK(dalloc(&s.k, cap * 8));
+  CK(dalloc(&s.key_slot, cap));
+  CK(dalloc(&s.key_index, cap));
+  CK(dalloc(&s.key_rep, cap));
+  CK(dalloc(&s.table, T));
+  CK(dalloc(&s.slot_key, T));
+  CK(dalloc(&s.pts, (1 + 2 * cap) * NIELS_WORDS));
+  CK(dalloc(&s.scal, (1 + 2 * cap) * 8));
+  CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
+  CK(dalloc(&s.u_acc, KEY_ACC_LIMBS));
+  CK(dalloc(&s.counts, NBIN));
+  CK(dalloc(&s.offsets, NBIN));
+  CK(dalloc(&s.cursor, NBIN));
+  CK(dalloc(&s.entries, msm_entry_capacity((uint32_t)cap)));
+  CK(dalloc(&s.slice_W, (size_t)NBIN * EXT_WORDS));
+  CK(dalloc(&s.slice_T, (size_t)NBIN * EXT_WORDS));
+  CK(dalloc(&s.win, (size_t)NWIN_FULL * EXT_WORDS));
+  CK(dalloc(&s.buckets, msm_bucket_words()));
+  launch_init_basepoint(s.st, s.pts);
+  CK(hipGetLastError());
+  s.cap_n = cap;
+  s.cap_T = T;
+  return 0;
+}
+
+// host-staging buffers (inputs of the host-pointer entry points, per-item outputs)
 static int ensure_n(edc_ctx* ctx, size_t n) {
-  if (n <= ctx->cap_n && ctx->pts) return 0;
-  CK(hipStreamSynchronize(ctx->st));
-  free_workspace(ctx);
-  size_t cap = n < 1024 ? 1024 : n + n / 8;
-  size_t T = next_pow2(2 * cap);
+  if (n <= ctx->cap_n && ctx->vk) return 0;
+  CK(hipStreamSynchronize(ctx->st()));
+  void* ptrs[] = {ctx->vk, ctx->sig, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  const size_t cap = n < 1024 ? 1024 : n + n / 8;
   CK(dalloc(&ctx->vk, cap * 32));
   CK(dalloc(&ctx->sig, cap * 64));
   CK(dalloc(&ctx->zexp, cap * 16));
   CK(dalloc(&ctx->off, cap + 1));
-  CK(dalloc(&ctx->k, cap * 8));
-  CK(dalloc(&ctx->key_slot, cap));
-  CK(dalloc(&ctx->key_index, cap));
-  CK(dalloc(&ctx->key_rep, cap));
-  CK(dalloc(&ctx->table, T));
-  CK(dalloc(&ctx->slot_key, T));
-  CK(dalloc(&ctx->pts, (1 + 2 * cap) * NIELS_WORDS));
-  CK(dalloc(&ctx->scal, (1 + 2 * cap) * 8));
-  CK(dalloc(&ctx->key_acc, cap * KEY_ACC_LIMBS));
-  CK(dalloc(&ctx->u_acc, KEY_ACC_LIMBS));
-  CK(dalloc(&ctx->counts, NBIN));
-  CK(dalloc(&ctx->offsets, NBIN));
-  CK(dalloc(&ctx->cursor, NBIN));
-  CK(dalloc(&ctx->entries, msm_entry_capacity((uint32_t)cap)));
-  CK(dalloc(&ctx->slice_W, (size_t)NBIN * EXT_WORDS));
-  CK(dalloc(&ctx->slice_T, (size_t)NBIN * EXT_WORDS));
-  CK(dalloc(&ctx->win, (size_t)NWIN_FULL * EXT_WORDS));
-  CK(dalloc(&ctx->buckets, msm_bucket_words()));
+  CK(dalloc(&ctx->kbuf, cap * 8));
   CK(dalloc(&ctx->verdicts, cap));
-  launch_init_basepoint(ctx->st, ctx->pts);
-  CK(hipGetLastError());
   ctx->cap_n = cap;
-  ctx->cap_T = T;
   return 0;
 }
 
 static int ensure_msg(edc_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->cap_msg && ctx->msg) return 0;
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipStreamSynchronize(ctx->st()));
   if (ctx->msg) (void)hipFree(ctx->msg);
   size_t cap = bytes < 4096 ? 4096 : bytes + bytes / 8;
   CK(dalloc(&ctx->msg, cap));
@@ -136,7 +167,7 @@ static int ensure_msg(edc_ctx* ctx, size_t bytes) {
 
 static int ensure_aux(edc_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->cap_aux && ctx->aux) return 0;
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipStreamSynchronize(ctx->st()));
   if (ctx->aux) (void)hipFree(ctx->aux);
   size_t cap = bytes < 4096 ? 4096 : bytes + bytes / 8;
   CK(dalloc(&ctx->aux, cap));
@@ -151,28 +182,27 @@ static void seed_words(const uint8_t* seed, uint32_t w[8]) {
                 : 0u;
 }
 
-static inline void mark(edc_ctx* ctx, int ph) {
-  if (ctx->timing) (void)hipEventRecord(ctx->ev[ph], ctx->st);
-}
-
-// Stage the message arena + offsets (0-based) into the context's device buffers.
+// Stage the message arena + offsets (0-based) into the context's device buffers (slot 0 stream).
 static int upload_msgs(edc_ctx* ctx, size_t n, const uint8_t* msg, const uint64_t* msg_off) {
   if (n && !msg_off) { ctx->err = "null msg_off"; return EDC_ERR_ARG; }
-  int rc = ensure_n(ctx, n);
+  int rc = init_slot(ctx, ctx->slot[0]);
+  if (rc) return rc;
+  rc = ensure_n(ctx, n);
   if (rc) return rc;
   const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
   if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
   rc = ensure_msg(ctx, mbytes);
   if (rc) return rc;
   if (!n) return 0;
-  if (mbytes) CK(hipMemcpyAsync(ctx->msg, msg + msg_off[0], mbytes, hipMemcpyHostToDevice, ctx->st));
+  hipStream_t st = ctx->st();
+  if (mbytes) CK(hipMemcpyAsync(ctx->msg, msg + msg_off[0], mbytes, hipMemcpyHostToDevice, st));
   if (msg_off[0] == 0) {
-    CK(hipMemcpyAsync(ctx->off, msg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->st));
+    CK(hipMemcpyAsync(ctx->off, msg_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   } else {
     std::vector<uint64_t> o(n + 1);
     for (size_t i = 0; i <= n; ++i) o[i] = msg_off[i] - msg_off[0];
-    CK(hipMemcpyAsync(ctx->off, o.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->st));
-    CK(hipStreamSynchronize(ctx->st));
+    CK(hipMemcpyAsync(ctx->off, o.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    CK(hipStreamSynchronize(st));
   }
   return 0;
 }
@@ -183,64 +213,83 @@ static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
   if (n && (!vk || !sig)) { ctx->err = "null input"; return EDC_ERR_ARG; }
   int rc = upload_msgs(ctx, n, msg, msg_off);
   if (rc || !n) return rc;
-  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st));
-  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st));
+  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st()));
+  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st()));
   return 0;
 }
 
-// The batch pipeline on device-resident inputs. Leaves the 256-byte result block in h_out.
-static int run_batch(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig, const uint8_t* d_msg,
-                     const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base, const uint8_t* d_z,
-                     int want_compress) {
+// Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
+static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                         const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
+                         const uint8_t* d_z, int want_compress) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
-  int rc = ensure_n(ctx, n);
+  int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
   const uint32_t N = (uint32_t)n;
   const uint32_t T = (uint32_t)next_pow2(2 * (n < 128 ? 128 : n));
-  if (T > ctx->cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
+  if (T > s.cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
   uint32_t seed[8];
   seed_words(z_seed, seed);
-  hipStream_t st = ctx->st;
-  CK(hipMemsetAsync(ctx->flags, 0, FLAG_COUNT * sizeof(int), st));
-  CK(hipMemsetAsync(ctx->table, 0xFF, (size_t)T * sizeof(uint32_t), st));
-  CK(hipMemsetAsync(ctx->u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
-  CK(hipMemsetAsync(ctx->d_out, 0, 256, st));
-  mark(ctx, PH_CHALLENGE);
-  launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, ctx->k);
-  mark(ctx, PH_DECOMP_R);
-  launch_decompress_R(st, N, d_sig, ctx->pts, ctx->flags);
-  mark(ctx, PH_KEYS);
-  launch_keys(st, N, d_vk, ctx->table, T - 1, seed[0] ^ 0x5bd1e995u, ctx->slot_key, ctx->key_slot,
-              ctx->key_rep, ctx->key_index, ctx->pts, ctx->key_acc, ctx->flags);
-  mark(ctx, PH_COEF);
-  launch_coef(st, N, d_sig, ctx->k, d_z, seed, z_base, ctx->key_index, ctx->scal, ctx->key_acc, ctx->u_acc,
-              ctx->flags);
-  mark(ctx, PH_MSM_BIN);
-  launch_msm_bin(st, N, ctx->scal, ctx->counts, ctx->offsets, ctx->cursor, ctx->entries, ctx->flags);
-  mark(ctx, PH_MSM_BUCKET);
-  launch_msm_bucket(st, ctx->counts, ctx->offsets, ctx->entries, ctx->pts, ctx->buckets, ctx->slice_W,
-                    ctx->slice_T);
-  mark(ctx, PH_MSM_TAIL);
-  launch_msm_tail(st, ctx->slice_W, ctx->slice_T, ctx->win, ctx->flags, want_compress, ctx->d_out);
-  mark(ctx, PH_N);
+  hipStream_t st = s.st;
+  s.timed = ctx->timing;
+  auto mark = [&](int ph) {
+    if (s.timed) (void)hipEventRecord(s.ev[ph], st);
+  };
+  CK(hipMemsetAsync(s.flags, 0, FLAG_COUNT * sizeof(int), st));
+  CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
+  CK(hipMemsetAsync(s.u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
+  CK(hipMemsetAsync(s.d_out, 0, 256, st));
+  mark(PH_CHALLENGE);
+  launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
+  mark(PH_DECOMP_R);
+  launch_decompress_R(st, N, d_sig, s.pts, s.flags);
+  mark(PH_KEYS);
+  launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
+              s.pts, s.key_acc, s.flags);
+  mark(PH_COEF);
+  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags);
+  mark(PH_MSM_BIN);
+  launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  mark(PH_MSM_BUCKET);
+  launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.pts, s.buckets, s.slice_W, s.slice_T);
+  mark(PH_MSM_TAIL);
+  launch_msm_tail(st, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
+  mark(PH_N);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(ctx->h_out, ctx->d_out, 256, hipMemcpyDeviceToHost, st));
-  CK(hipStreamSynchronize(st));
-  if (ctx->timing) {
-    for (int p = 0; p < PH_N; ++p) CK(hipEventElapsedTime(&ctx->last_ms[p], ctx->ev[p], ctx->ev[p + 1]));
-    ctx->nlast = PH_N;
-  }
+  CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, st));
+  s.pending = true;
   return 0;
 }
 
-static int verdict_from_out(edc_ctx* ctx, uint8_t check8[32]) {
-  int verdict = reinterpret_cast<int*>(ctx->h_out)[0];
-  int bad = reinterpret_cast<int*>(ctx->h_out)[1];
+// Wait for slot s and harvest its result block (verdict, bad flag, check8, partial).
+static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t partial[128], int* bad_out) {
+  if (!s.pending) { ctx->err = "no batch pending in this slot"; return EDC_ERR_ARG; }
+  s.pending = false;
+  CK(hipStreamSynchronize(s.st));
+  if (s.timed) {
+    for (int p = 0; p < PH_N; ++p) CK(hipEventElapsedTime(&ctx->last_ms[p], s.ev[p], s.ev[p + 1]));
+    ctx->nlast = PH_N;
+  }
+  const int verdict = reinterpret_cast<int*>(s.h_out)[0];
+  const int bad = reinterpret_cast<int*>(s.h_out)[1];
   if (check8) {
     if (bad) memset(check8, 0, 32);
-    else memcpy(check8, ctx->h_out + 16, 32);
+    else memcpy(check8, s.h_out + 16, 32);
   }
+  if (partial) memcpy(partial, s.h_out + 48, 128);
+  if (bad_out) *bad_out = bad;
   return verdict ? EDC_INVALID_SIGNATURE : EDC_OK;
+}
+
+// Synchronous batch on slot 0.
+static int run_batch_sync(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig, const uint8_t* d_msg,
+                          const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base, const uint8_t* d_z,
+                          uint8_t check8[32], uint8_t partial[128], int* bad) {
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
+  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, check8 != nullptr);
+  if (rc) return rc;
+  return finish_batch(ctx, s, check8, partial, bad);
 }
 
 extern "C" {
@@ -254,16 +303,11 @@ int edc_device_count(void) {
 edc_ctx* edc_create(int device) {
   edc_ctx* ctx = new edc_ctx();
   ctx->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
-    delete ctx;
-    return nullptr;
-  }
-  bool ok = dalloc(&ctx->btab, 8 * NIELS_WORDS) == hipSuccess && dalloc(&ctx->flags, FLAG_COUNT) == hipSuccess &&
-            dalloc(&ctx->d_out, 256) == hipSuccess && hipHostMalloc((void**)&ctx->h_out, 256) == hipSuccess;
-  for (int p = 0; ok && p <= PH_N; ++p) ok = hipEventCreate(&ctx->ev[p]) == hipSuccess;
+  bool ok = hipSetDevice(device) == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
+            dalloc(&ctx->btab, 8 * NIELS_WORDS) == hipSuccess;
   if (ok) {
-    launch_init_btable(ctx->st, ctx->btab);
-    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->st) == hipSuccess;
+    launch_init_btable(ctx->st(), ctx->btab);
+    ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->st()) == hipSuccess;
   }
   if (!ok) {
     edc_destroy(ctx);
@@ -275,17 +319,19 @@ edc_ctx* edc_create(int device) {
 void edc_destroy(edc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->st) (void)hipStreamSynchronize(ctx->st);
-  free_workspace(ctx);
-  if (ctx->msg) (void)hipFree(ctx->msg);
-  if (ctx->aux) (void)hipFree(ctx->aux);
-  if (ctx->btab) (void)hipFree(ctx->btab);
-  if (ctx->flags) (void)hipFree(ctx->flags);
-  if (ctx->d_out) (void)hipFree(ctx->d_out);
-  if (ctx->h_out) (void)hipHostFree(ctx->h_out);
-  for (int p = 0; p <= PH_N; ++p)
-    if (ctx->ev[p]) (void)hipEventDestroy(ctx->ev[p]);
-  if (ctx->st) (void)hipStreamDestroy(ctx->st);
+  for (Slot& s : ctx->slot) {
+    if (s.st) (void)hipStreamSynchronize(s.st);
+    free_slot_buffers(s);
+    if (s.flags) (void)hipFree(s.flags);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    for (int p = 0; p <= PH_N; ++p)
+      if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
+    if (s.st) (void)hipStreamDestroy(s.st);
+  }
+  void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->aux, ctx->btab};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
   delete ctx;
 }
 
@@ -297,9 +343,7 @@ int edc_batch_verify(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* s
   CK(hipSetDevice(ctx->device));
   int rc = upload(ctx, n, vk, sig, msg, msg_off);
   if (rc) return rc;
-  rc = run_batch(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, z_seed, 0, nullptr, check8 != nullptr);
-  if (rc) return rc;
-  return verdict_from_out(ctx, check8);
+  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, z_seed, 0, nullptr, check8, nullptr, nullptr);
 }
 
 int edc_batch_verify_z(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
@@ -308,10 +352,9 @@ int edc_batch_verify_z(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t*
   CK(hipSetDevice(ctx->device));
   int rc = upload(ctx, n, vk, sig, msg, msg_off);
   if (rc) return rc;
-  if (n) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, ctx->st));
-  rc = run_batch(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, nullptr, 0, ctx->zexp, check8 != nullptr);
-  if (rc) return rc;
-  return verdict_from_out(ctx, check8);
+  if (n) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, ctx->st()));
+  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, nullptr, 0, ctx->zexp, check8, nullptr,
+                        nullptr);
 }
 
 int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
@@ -319,9 +362,30 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
                             uint64_t z_base, const uint8_t* d_z, uint8_t check8[32]) {
   if (!ctx || (!z_seed && !d_z)) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  int rc = run_batch(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, check8 != nullptr);
+  return run_batch_sync(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, check8, nullptr, nullptr);
+}
+
+int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                                uint64_t z_base, const uint8_t* d_z, int want_check8) {
+  if (!ctx || (!z_seed && !d_z)) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % kSlots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, want_check8 != 0);
   if (rc) return rc;
-  return verdict_from_out(ctx, check8);
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad) {
+  if (!ctx || ticket < 0) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  Slot& s = ctx->slot[ticket % kSlots];
+  if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
+  return finish_batch(ctx, s, check8, partial, bad);
 }
 
 int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
@@ -329,11 +393,8 @@ int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const 
                              uint64_t z_base, const uint8_t* d_z, uint8_t partial[128], int* bad) {
   if (!ctx || !partial || (!z_seed && !d_z)) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  int rc = run_batch(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, 0);
-  if (rc) return rc;
-  memcpy(partial, ctx->h_out + 48, 128);
-  if (bad) *bad = reinterpret_cast<int*>(ctx->h_out)[1];
-  return 0;
+  int rc = run_batch_sync(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, nullptr, partial, bad);
+  return rc < 0 ? rc : 0;
 }
 
 int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad_any, uint8_t check8[32]) {
@@ -341,13 +402,16 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
   CK(hipSetDevice(ctx->device));
   int rc = ensure_aux(ctx, g * 128 + 1);
   if (rc) return rc;
-  if (g) CK(hipMemcpyAsync(ctx->aux, partials, g * 128, hipMemcpyHostToDevice, ctx->st));
-  CK(hipMemsetAsync(ctx->d_out, 0, 256, ctx->st));
-  launch_combine(ctx->st, (uint32_t)g, ctx->aux, bad_any ? 1 : 0, check8 != nullptr, ctx->d_out);
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy"; return EDC_ERR_ARG; }
+  if (g) CK(hipMemcpyAsync(ctx->aux, partials, g * 128, hipMemcpyHostToDevice, s.st));
+  CK(hipMemsetAsync(s.d_out, 0, 256, s.st));
+  launch_combine(s.st, (uint32_t)g, ctx->aux, bad_any ? 1 : 0, check8 != nullptr, s.d_out);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(ctx->h_out, ctx->d_out, 256, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
-  return verdict_from_out(ctx, check8);
+  CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, s.st));
+  s.pending = true;
+  s.timed = false;
+  return finish_batch(ctx, s, check8, nullptr, nullptr);
 }
 
 int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
@@ -357,10 +421,10 @@ int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
   int rc = upload(ctx, n, vk, sig, msg, msg_off);
   if (rc) return rc;
   if (!n) return 0;
-  launch_challenge(ctx->st, (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->k);
+  launch_challenge(ctx->st(), (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->kbuf);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(k_out, ctx->k, n * 32, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipMemcpyAsync(k_out, ctx->kbuf, n * 32, hipMemcpyDeviceToHost, ctx->st()));
+  CK(hipStreamSynchronize(ctx->st()));
   return 0;
 }
 
@@ -371,13 +435,14 @@ int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const u
   int rc = ensure_n(ctx, n);
   if (rc) return rc;
   if (!n) return 0;
-  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st));
-  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st));
-  CK(hipMemcpyAsync(ctx->k, k, n * 32, hipMemcpyHostToDevice, ctx->st));
-  launch_verify_single(ctx->st, (uint32_t)n, ctx->vk, ctx->sig, ctx->k, ctx->btab, ctx->verdicts);
+  hipStream_t st = ctx->st();
+  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(ctx->kbuf, k, n * 32, hipMemcpyHostToDevice, st));
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -388,11 +453,12 @@ int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* si
   int rc = upload(ctx, n, vk, sig, msg, msg_off);
   if (rc) return rc;
   if (!n) return 0;
-  launch_challenge(ctx->st, (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->k);
-  launch_verify_single(ctx->st, (uint32_t)n, ctx->vk, ctx->sig, ctx->k, ctx->btab, ctx->verdicts);
+  hipStream_t st = ctx->st();
+  launch_challenge(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->kbuf);
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -404,12 +470,13 @@ int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint
   rc = ensure_aux(ctx, n * 64);
   if (rc) return rc;
   if (!n) return 0;
-  CK(hipMemcpyAsync(ctx->vk, enc, n * 32, hipMemcpyHostToDevice, ctx->st));
-  launch_decode(ctx->st, (uint32_t)n, ctx->vk, ctx->aux, ctx->verdicts);
+  hipStream_t st = ctx->st();
+  CK(hipMemcpyAsync(ctx->vk, enc, n * 32, hipMemcpyHostToDevice, st));
+  launch_decode(st, (uint32_t)n, ctx->vk, ctx->aux, ctx->verdicts);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(xy, ctx->aux, n * 64, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipMemcpyAsync(ok, ctx->verdicts, n, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipMemcpyAsync(xy, ctx->aux, n * 64, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(ok, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -417,9 +484,9 @@ int edc_sign_device(edc_ctx* ctx, size_t n, const uint8_t* d_seeds, const uint32
                     const uint8_t* d_msg, const uint64_t* d_msg_off, uint8_t* d_vk_out, uint8_t* d_sig_out) {
   if (!ctx) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  launch_sign(ctx->st, (uint32_t)n, d_seeds, d_seed_index, d_msg, d_msg_off, ctx->btab, d_vk_out, d_sig_out);
+  launch_sign(ctx->st(), (uint32_t)n, d_seeds, d_seed_index, d_msg, d_msg_off, ctx->btab, d_vk_out, d_sig_out);
   CK(hipGetLastError());
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipStreamSynchronize(ctx->st()));
   return 0;
 }
 
@@ -438,20 +505,22 @@ int edc_sign(edc_ctx* ctx, size_t n, const uint8_t* seeds, size_t nseeds, const 
   if (rc) return rc;
   if (!n) return 0;
   // aux: seeds (nseeds*32) | seed_index (n*4) | vk_out (n*32) | sig_out (n*64)
-  size_t sb = nseeds * 32, ib = seed_index ? n * 4 : 0;
-  rc = ensure_aux(ctx, sb + ib + n * 96 + 64);
+  const size_t sb = nseeds * 32, ib = seed_index ? n * 4 : 0;
+  const size_t sb16 = (sb + 15) & ~(size_t)15, ib16 = (ib + 15) & ~(size_t)15;
+  rc = ensure_aux(ctx, sb16 + ib16 + n * 96 + 64);
   if (rc) return rc;
+  hipStream_t st = ctx->st();
   uint8_t* d_seeds = ctx->aux;
-  uint32_t* d_idx = seed_index ? reinterpret_cast<uint32_t*>(ctx->aux + ((sb + 15) & ~(size_t)15)) : nullptr;
-  uint8_t* d_vk = ctx->aux + ((sb + 15) & ~(size_t)15) + ((ib + 15) & ~(size_t)15);
+  uint32_t* d_idx = seed_index ? reinterpret_cast<uint32_t*>(ctx->aux + sb16) : nullptr;
+  uint8_t* d_vk = ctx->aux + sb16 + ib16;
   uint8_t* d_sig = d_vk + n * 32;
-  CK(hipMemcpyAsync(d_seeds, seeds, sb, hipMemcpyHostToDevice, ctx->st));
-  if (d_idx) CK(hipMemcpyAsync(d_idx, seed_index, ib, hipMemcpyHostToDevice, ctx->st));
-  launch_sign(ctx->st, (uint32_t)n, d_seeds, d_idx, ctx->msg, ctx->off, ctx->btab, d_vk, d_sig);
+  CK(hipMemcpyAsync(d_seeds, seeds, sb, hipMemcpyHostToDevice, st));
+  if (d_idx) CK(hipMemcpyAsync(d_idx, seed_index, ib, hipMemcpyHostToDevice, st));
+  launch_sign(st, (uint32_t)n, d_seeds, d_idx, ctx->msg, ctx->off, ctx->btab, d_vk, d_sig);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(vk_out, d_vk, n * 32, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipMemcpyAsync(sig_out, d_sig, n * 64, hipMemcpyDeviceToHost, ctx->st));
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipMemcpyAsync(vk_out, d_vk, n * 32, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(sig_out, d_sig, n * 64, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
   return 0;
 }
 
@@ -460,9 +529,9 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
   CK(hipSetDevice(ctx->device));
   uint32_t k[8];
   seed_words(key, k);
-  launch_chacha_fill(ctx->st, k, blk0, nblocks, reinterpret_cast<uint32_t*>(d_out));
+  launch_chacha_fill(ctx->st(), k, blk0, nblocks, reinterpret_cast<uint32_t*>(d_out));
   CK(hipGetLastError());
-  CK(hipStreamSynchronize(ctx->st));
+  CK(hipStreamSynchronize(ctx->st()));
   return 0;
 }
 
@@ -482,7 +551,8 @@ const char* edc_timing_name(int i) { return (i >= 0 && i < PH_N) ? kPhaseNames[i
 int edc_synchronize(edc_ctx* ctx) {
   if (!ctx) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  CK(hipStreamSynchronize(ctx->st));
+  for (Slot& s : ctx->slot)
+    if (s.st) CK(hipStreamSynchronize(s.st));
   return 0;
 }
 

@@ -171,14 +171,13 @@ __device__ __forceinline__ void weighted_sum_256(const uint32_t* lds_pts, uint32
   // two trees: R (sum of res_g) and S (sum of suffixes), interleaved per step
   for (int d = 32; d >= 1; d >>= 1) {
     __syncthreads();
+    ge_p3 x, y;
     if (g < d) {
-      ge_p3 x = quad_add(ld_ext(R + g * EXT_WORDS), ld_ext(R + (g + d) * EXT_WORDS));
-      ge_p3 y = quad_add(ld_ext(S + g * EXT_WORDS), ld_ext(S + (g + d) * EXT_WORDS));
-      __syncthreads();
-      if (leader) { st_ext(R + g * EXT_WORDS, x); st_ext(S + g * EXT_WORDS, y); }
-    } else {
-      __syncthreads();
+      x = quad_add(ld_ext(R + g * EXT_WORDS), ld_ext(R + (g + d) * EXT_WORDS));
+      y = quad_add(ld_ext(S + g * EXT_WORDS), ld_ext(S + (g + d) * EXT_WORDS));
     }
+    __syncthreads();   // every lane reaches both barriers: none sits in a divergent branch
+    if (g < d && leader) { st_ext(R + g * EXT_WORDS, x); st_ext(S + g * EXT_WORDS, y); }
   }
   __syncthreads();
   if (g == 0) wsum = quad_add(ld_ext(R), quad_dbl(quad_dbl(ld_ext(S))));

@@ -74,7 +74,9 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
   ld_words8(vk + (size_t)i * 32, w);
   uint32_t h = key_hash(w, salt) & tmask;
   for (uint32_t probe = 0; probe <= tmask; ++probe) {
-    uint32_t cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // plain (L1-cached) first probe: a slot never changes once claimed, and a stale EMPTY is
+    // resolved by the CAS below, so the hot validator slots are served from L1
+    uint32_t cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (cur == 0xFFFFFFFFu) {
       uint32_t prev = atomicCAS(&table[h], 0xFFFFFFFFu, i);
       if (prev == 0xFFFFFFFFu) {

@@ -75,6 +75,20 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
                             uint8_t check8[32]);
 
 /*
+ * Asynchronous form of edc_batch_verify_device for streams of batches (a consensus node
+ * verifying block after block): edc_batch_submit_device enqueues the whole pipeline on one of the
+ * context's in-flight slots (2) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
+ * ticket and returns its verdict (EDC_OK / EDC_INVALID_SIGNATURE, <0 on runtime failure), with
+ * optional check8 (needs want_check8), partial point and bad flag. Tickets must be waited in
+ * submission order before their slot is reused; inputs must stay valid until the wait.
+ */
+int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                const uint8_t* d_msg, const uint64_t* d_msg_off,
+                                const uint8_t z_seed[32], uint64_t z_base, const uint8_t* d_z,
+                                int want_check8);
+int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad);
+
+/*
  * Multi-GPU shard: evaluate this shard's part of the batch equation WITHOUT the cofactor /
  * identity step. partial (128 bytes) = canonical X||Y||Z||T of the shard's check point;
  * *bad = 1 if any item of the shard failed decoding / canonicity. Items are the shard's slice

@@ -210,3 +210,45 @@ def test_large_batch_properties(engine):
     assert code == 1
     v = engine.verify_each(vks, sigs, msgs2)
     assert [i for i, c in enumerate(v) if c] == [bad]
+
+
+def test_async_submit_wait_two_in_flight(engine, edc):
+    """edc_batch_submit_device / edc_batch_wait: two batches in flight on separate slots give the
+    same verdicts and [8]*check as the synchronous path."""
+    import ctypes
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    bs = {x["name"]: x for x in golden("batches.json")["batches"]}
+    jobs = []
+    for name in ["two_bad_of_300", "repeated_keys_varlen", "mixed_corpus_one_bad", "c1_1024_distinct"]:
+        b = bs[name]
+        it = _items(b)
+        vk = torch.tensor(list(b"".join(v for v, _, _ in it)), dtype=torch.uint8, device=dev)
+        sg = torch.tensor(list(b"".join(s for _, s, _ in it)), dtype=torch.uint8, device=dev)
+        ms = torch.tensor(list(b"".join(m for _, _, m in it)) or [0], dtype=torch.uint8, device=dev)
+        offs = [0]
+        for _, _, m in it:
+            offs.append(offs[-1] + len(m))
+        off = torch.tensor(offs, dtype=torch.int64, device=dev)
+        jobs.append((b, len(it), vk, sg, ms, off))
+    torch.cuda.synchronize()
+    lib = engine.lib
+    tickets = []
+    results = []
+    for b, n, vk, sg, ms, off in jobs:
+        if len(tickets) == 2:
+            t0, b0 = tickets.pop(0)
+            c8 = ctypes.create_string_buffer(32)
+            results.append((b0, lib.edc_batch_wait(engine.ctx, t0, c8, None, None), c8.raw))
+        t = lib.edc_batch_submit_device(engine.ctx, n, vk.data_ptr(), sg.data_ptr(), ms.data_ptr(), off.data_ptr(),
+                                        bytes.fromhex(b["z_seed"]), 0, None, 1)
+        assert t >= 0
+        tickets.append((t, b))
+    while tickets:
+        t0, b0 = tickets.pop(0)
+        c8 = ctypes.create_string_buffer(32)
+        results.append((b0, lib.edc_batch_wait(engine.ctx, t0, c8, None, None), c8.raw))
+    assert len(results) == 4
+    for b, code, c8 in results:
+        assert code == b["expect_code"], b["name"]
+        assert c8.hex() == b["expect_check8"], b["name"]
