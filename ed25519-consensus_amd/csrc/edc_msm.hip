@@ -206,7 +206,7 @@ constexpr int BKT_CHUNK = 4096;
 // one workgroup per bin (window w, slice s), one lane per bucket: S_b for b = 256 s + t + 1.
 // Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK), then lane t walks its
 // bucket's entries with the next Niels point prefetched under the current 7M mixed addition.
-__global__ void __launch_bounds__(256) k_msm_accum(const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict__ counts,
                                                    const uint32_t* __restrict__ offsets,
                                                    const uint2* __restrict__ entries,
                                                    const uint32_t* __restrict__ pts,

@@ -14,7 +14,7 @@
 
 namespace edc {
 
-__global__ void __launch_bounds__(256) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
+__global__ void __launch_bounds__(256, 4) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
                                                    const uint8_t* __restrict__ sig,
                                                    const uint8_t* __restrict__ msg,
                                                    const uint64_t* __restrict__ off,
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) k_challenge(uint32_t n, const uint8_t* __
 }
 
 // R_i -> points[1 + i]
-__global__ void __launch_bounds__(256) k_decompress_R(uint32_t n, const uint8_t* __restrict__ sig,
+__global__ void __launch_bounds__(256, 4) k_decompress_R(uint32_t n, const uint8_t* __restrict__ sig,
                                                       uint32_t* __restrict__ pts,
                                                       int* __restrict__ flags) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) k_key_index(uint32_t n, const uint32_t* _
 }
 
 // distinct key j -> points[1 + n + j]
-__global__ void __launch_bounds__(256) k_decompress_A(uint32_t n, const uint8_t* __restrict__ vk,
+__global__ void __launch_bounds__(256, 4) k_decompress_A(uint32_t n, const uint8_t* __restrict__ vk,
                                                       const uint32_t* __restrict__ key_rep,
                                                       uint32_t* __restrict__ pts,
                                                       int* __restrict__ flags) {
