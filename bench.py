@@ -211,10 +211,11 @@ def main():
         total = n * world * args.steps
         value = total / elapsed
         ms_per_step = elapsed / args.steps * 1e3
-        dom_ms = phases["decompress_R"]
-        achieved = n * ALG_MAD_DECOMP / (dom_ms * 1e-3) / 1e12
+        dom_ms = phases["decompress_R_and_keys"]
+        units = n + args.keys          # R_i of every signature + every distinct key, one launch
+        achieved = units * ALG_MAD_DECOMP / (dom_ms * 1e-3) / 1e12
         traffic = None
-        tpath = os.path.join(ROOT, "profiles", "traffic_decompress_R.json")
+        tpath = os.path.join(ROOT, "profiles", "traffic_k_decompress.json")
         if os.path.exists(tpath):
             try:
                 t = json.load(open(tpath))
@@ -242,11 +243,11 @@ def main():
                        "sigs_per_gpu": n, "validators": args.keys, "msg_len": args.msg_len,
                        "inflight": args.inflight if world == 1 else 1,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
-            "roofline": {"bound": "valu_int", "kernel": "k_decompress_R",
+            "roofline": {"bound": "valu_int", "kernel": "k_decompress",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
                          "traffic": traffic,
-                         "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": n,
+                         "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": units,
                          "avg_launch_ms": dom_ms},
             "phases_ms": phases,
             "cpu_baseline": cpu,

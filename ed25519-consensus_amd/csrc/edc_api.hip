@@ -11,8 +11,9 @@ using namespace edc;
 
 namespace {
 
-enum Phase { PH_CHALLENGE, PH_DECOMP_R, PH_KEYS, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
-const char* kPhaseNames[PH_N] = {"challenge_sha512", "decompress_R", "keys_group_decompress_A",
+// phases in enqueue order (each bracketed by HIP events on the slot stream)
+enum Phase { PH_CHALLENGE, PH_KEYS, PH_DECOMP, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
+const char* kPhaseNames[PH_N] = {"challenge_sha512", "keys_group", "decompress_R_and_keys",
                                  "coef_chacha_scalar", "msm_bin", "msm_bucket", "msm_window_final"};
 
 template <typename T>
@@ -241,11 +242,11 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   CK(hipMemsetAsync(s.d_out, 0, 256, st));
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
-  mark(PH_DECOMP_R);
-  launch_decompress_R(st, N, d_sig, s.pts, s.flags);
   mark(PH_KEYS);
   launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
               s.pts, s.key_acc, s.flags);
+  mark(PH_DECOMP);
+  launch_decompress(st, N, d_sig, d_vk, s.key_rep, s.pts, s.flags);
   mark(PH_COEF);
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags);
   mark(PH_MSM_BIN);

@@ -7,7 +7,8 @@ namespace edc {
 // edc_prep.hip
 void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
-void launch_decompress_R(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
+                       uint32_t* pts, int* flags);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
                  uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);

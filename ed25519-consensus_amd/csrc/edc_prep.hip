@@ -2,10 +2,9 @@
 // (reference src/batch.rs:82-94 queue-time hashing, :174-203 the decode/coefficient loop).
 //
 //   k_challenge     k_i = SHA-512(R_i || A_i || M_i) mod l                (K1)
-//   k_decompress_R  ZIP215 decode of R_i -> affine Niels point             (K2)
 //   k_key_insert    group signatures by raw key bytes (HashMap<VerificationKeyBytes,..>)
 //   k_key_index     dense key index per signature
-//   k_decompress_A  ZIP215 decode of each distinct key                      (K2)
+//   k_decompress    ZIP215 decode of every R_i and every distinct key -> affine Niels (K2)
 //   k_coef          z_i (ChaCha20), s_i < l check, u_i = z_i s_i, v_i = z_i k_i,
 //                   per-key and global 64-bit limb sums                      (K3)
 //   k_key_final     A_coeff = sum v_i mod l per key; B_coeff = -sum u_i mod l
@@ -31,16 +30,26 @@ __global__ void __launch_bounds__(256, 4) k_challenge(uint32_t n, const uint8_t*
   kp[1] = make_uint4(k.v[4], k.v[5], k.v[6], k.v[7]);
 }
 
-// R_i -> points[1 + i]
-__global__ void __launch_bounds__(256, 4) k_decompress_R(uint32_t n, const uint8_t* __restrict__ sig,
-                                                      uint32_t* __restrict__ pts,
-                                                      int* __restrict__ flags) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// One launch decodes both the signatures' R_i (threads [0, n) -> points[1 + i]) and the distinct
+// keys (threads [n, n + m) -> points[1 + n + j]), so the few-key case (m = 150 validators) rides
+// along with the R decodes instead of paying a serial single-wave launch of its own.
+__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
+                                                       const uint8_t* __restrict__ vk,
+                                                       const uint32_t* __restrict__ key_rep,
+                                                       uint32_t* __restrict__ pts, int* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint8_t* enc;
+  if (i < n) {
+    enc = sig + (size_t)i * 64;
+  } else {
+    const uint32_t j = i - n;
+    if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
+    enc = vk + (size_t)key_rep[j] * 32;
+  }
   uint32_t w[8];
-  ld_words8(sig + (size_t)i * 64, w);
+  ld_words8(enc, w);
   ge_p3 P;
-  bool ok = ge_decompress(w, P);
+  const bool ok = ge_decompress(w, P);
   st_niels(pts, 1 + i, ge_to_niels_affine(P));
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
@@ -109,22 +118,6 @@ __global__ void __launch_bounds__(256) k_key_index(uint32_t n, const uint32_t* _
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   key_index[i] = slot_key[key_slot_of_sig[i]];
-}
-
-// distinct key j -> points[1 + n + j]
-__global__ void __launch_bounds__(256, 4) k_decompress_A(uint32_t n, const uint8_t* __restrict__ vk,
-                                                      const uint32_t* __restrict__ key_rep,
-                                                      uint32_t* __restrict__ pts,
-                                                      int* __restrict__ flags) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  if (j >= m) return;
-  uint32_t w[8];
-  ld_words8(vk + (size_t)key_rep[j] * 32, w);
-  ge_p3 P;
-  bool ok = ge_decompress(w, P);
-  st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
-  if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
 
 struct seed8 { uint32_t w[8]; };
@@ -302,8 +295,10 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k) {
   if (n) hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, sig, msg, off, k);
 }
-void launch_decompress_R(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags) {
-  if (n) hipLaunchKernelGGL(k_decompress_R, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
+                       uint32_t* pts, int* flags) {
+  // grid covers n R points + up to n distinct keys (m is read on the device)
+  if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(2ull * n, 256)), dim3(256), 0, st, n, sig, vk, key_rep, pts, flags);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
@@ -313,7 +308,6 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
                      slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index);
-  hipLaunchKernelGGL(k_decompress_A, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags);
 }
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
