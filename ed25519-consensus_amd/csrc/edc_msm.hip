@@ -204,23 +204,28 @@ __device__ __forceinline__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
 constexpr int BKT_CHUNK = 4096;
 
 // one workgroup per bin (window w, slice s), one lane per bucket: S_b for b = 256 s + t + 1.
-// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK), then lane t walks its
-// bucket's entries with the next Niels point prefetched under the current 7M mixed addition.
+// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK). Bucket sizes are
+// Poisson-distributed, and a wave runs as long as its fullest lane, so lanes take buckets in
+// order of decreasing entry count (LDS counting sort of the 256 counts): the buckets of one wave
+// then hold nearly equal work. Each lane walks its bucket with the next Niels point prefetched
+// under the current 7M mixed addition.
 __global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict__ counts,
-                                                   const uint32_t* __restrict__ offsets,
-                                                   const uint2* __restrict__ entries,
-                                                   const uint32_t* __restrict__ pts,
-                                                   uint32_t* __restrict__ buckets) {
+                                                      const uint32_t* __restrict__ offsets,
+                                                      const uint2* __restrict__ entries,
+                                                      const uint32_t* __restrict__ pts,
+                                                      uint32_t* __restrict__ buckets) {
   __shared__ uint32_t lidx[BKT_CHUNK];
   __shared__ uint32_t lcnt[NSLICE];
   __shared__ uint32_t lstart[NSLICE];
   __shared__ uint32_t lcur[NSLICE];
+  __shared__ uint32_t lorder[NSLICE];   // bucket handled by lane t (by decreasing count)
   const int t = threadIdx.x;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
   if (E == 0) return;
   const uint32_t off = offsets[bin];
   ge_p3 acc = ge_identity();
+  uint32_t my_bucket = t;
   for (uint32_t c0 = 0; c0 < E; c0 += BKT_CHUNK) {
     const uint32_t ch = min((uint32_t)BKT_CHUNK, E - c0);
     lcnt[t] = 0;
@@ -241,14 +246,25 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lstart[4 * t + j] = run; lcur[4 * t + j] = run; run += c[j]; }
     }
+    if (c0 == 0) {
+      // rank bucket t by (count desc, index): lanes of a wave get similar counts
+      const uint32_t mine = lcnt[t];
+      uint32_t rank = 0;
+      for (int u = 0; u < NSLICE; ++u) {
+        const uint32_t o = lcnt[u];
+        rank += (o > mine) || (o == mine && u < t);
+      }
+      lorder[rank] = t;
+    }
     __syncthreads();
+    if (c0 == 0) my_bucket = lorder[t];
     for (uint32_t e = t; e < ch; e += 256) {
       uint2 en = entries[off + c0 + e];
       uint32_t pos = atomicAdd(&lcur[en.y], 1u);
       lidx[pos] = en.x;
     }
     __syncthreads();
-    const uint32_t beg = lstart[t], cnt = lcnt[t];
+    const uint32_t beg = lstart[my_bucket], cnt = lcnt[my_bucket];
     if (cnt) {
       uint32_t e = lidx[beg];
       ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
@@ -263,7 +279,7 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict
     }
     __syncthreads();
   }
-  st_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS, acc);
+  st_ext(buckets + ((size_t)bin * NSLICE + my_bucket) * EXT_WORDS, acc);
 }
 
 // one workgroup per bin: W_s = sum_t (t+1) S_t and T_s = sum_t S_t (quad-cooperative)
