@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (submit/wait pipelining)")
+    ap.add_argument("--probe", action="store_true", help="measurement-probe builds: do not require Ok verdicts")
     args = ap.parse_args()
 
     import torch
@@ -189,7 +190,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    assert all(c == 0 for c in codes), f"valid synthetic batch rejected: {codes}"
+    if not args.probe:
+        assert all(c == 0 for c in codes), f"valid synthetic batch rejected: {codes}"
 
     # instrumented steps (outside the timed region): per-phase HIP-event timings on the
     # context stream, for the roofline of the dominant kernel

@@ -80,7 +80,8 @@ def load_library(path=None):
     with _lib_lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        # EDC_LIB_PATH: measurement hook to load an A/B variant build of the same sources
+        p = path or os.environ.get("EDC_LIB_PATH") or LIB_PATH
         if not os.path.exists(p):
             raise EngineError(f"HIP extension not built: {p} (run __graft_entry__.build())")
         _share_torch_hip_runtime()

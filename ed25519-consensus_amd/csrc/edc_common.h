@@ -11,8 +11,10 @@
 namespace edc {
 
 // ---- HBM record layouts ----
-// affine Niels point: ypx | ymx | xy2d as 9 radix-2^29 limbs each, padded to 28 words (112 B)
-constexpr int NIELS_WORDS = 28;
+// affine Niels point: ypx | ymx | xy2d as 9 radix-2^29 limbs each (27 words), padded to 32 words
+// so that every record is exactly one 128-byte cache line: the MSM gathers points in random
+// order, and a 112-byte record straddled two lines most of the time.
+constexpr int NIELS_WORDS = 32;
 // extended point: X | Y | Z | T, 36 words (144 B)
 constexpr int EXT_WORDS = 36;
 

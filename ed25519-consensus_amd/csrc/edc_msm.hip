@@ -139,7 +139,8 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
 //   returns (sum_t t * P_t, sum_t P_t), valid in quad 0 (threads 0..3).
 // Quad g folds points 4g..4g+3 (res_g = P1 + 2P2 + 3P3, run_g = sum), then a Hillis-Steele
 // suffix scan of run over the 64 quads gives sum_g 4g run_g = 4 sum_{g>=1} Suf_g; two trees
-// finish. Serial depth: 5 + 6 + 2*6 + 3 quad point ops. R and S are 64-point LDS scratch.
+// finish. Serial depth: 5 + 6 + 2*6 + 3 quad point ops. R and S are 64-point LDS scratch; they
+// may alias lds_pts (every point is read before the first scratch write).
 __device__ __forceinline__ void weighted_sum_256(const uint32_t* lds_pts, uint32_t* R, uint32_t* S, ge_p3& wsum, ge_p3& tot) {
   const int g = threadIdx.x >> 2;
   const bool leader = (threadIdx.x & 3) == 0;
@@ -203,34 +204,52 @@ __device__ __forceinline__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
 
 constexpr int BKT_CHUNK = 4096;
 
-// one workgroup per bin (window w, slice s), one lane per bucket: S_b for b = 256 s + t + 1.
-// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK). Bucket sizes are
-// Poisson-distributed, and a wave runs as long as its fullest lane, so lanes take buckets in
-// order of decreasing entry count (LDS counting sort of the 256 counts): the buckets of one wave
-// then hold nearly equal work. Each lane walks its bucket with the next Niels point prefetched
-// under the current 7M mixed addition.
-__global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict__ counts,
-                                                      const uint32_t* __restrict__ offsets,
-                                                      const uint2* __restrict__ entries,
-                                                      const uint32_t* __restrict__ pts,
-                                                      uint32_t* __restrict__ buckets) {
+// one workgroup per bin (window w, slice s) of 256 buckets: S_b for b = 256 s + t + 1.
+// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK). ACC_LANES lanes share
+// a bucket (lane group (t, t + 256, ...) walks entries j = half, half + ACC_LANES, ...; the group
+// is summed at the end), which shortens the serial chains of the dense bins. Bucket sizes are
+// Poisson-distributed and a wave runs as long as its fullest lane, so buckets are handed to lanes
+// in order of decreasing entry count. With ACC_PREFETCH the next Niels point is loaded under the
+// current 7M mixed addition.
+#ifndef EDC_ACC_LANES
+#define EDC_ACC_LANES 1
+#endif
+#ifndef EDC_ACC_PREFETCH
+#define EDC_ACC_PREFETCH 1
+#endif
+#ifndef EDC_ACC_WAVES
+#define EDC_ACC_WAVES 4
+#endif
+constexpr int ACC_LANES = EDC_ACC_LANES;
+constexpr int ACC_THREADS = ACC_LANES * NSLICE;
+
+__global__ void __launch_bounds__(ACC_THREADS, EDC_ACC_WAVES) k_msm_accum(const uint32_t* __restrict__ counts,
+                                                              const uint32_t* __restrict__ offsets,
+                                                              const uint2* __restrict__ entries,
+                                                              const uint32_t* __restrict__ pts,
+                                                              uint32_t* __restrict__ buckets) {
   __shared__ uint32_t lidx[BKT_CHUNK];
   __shared__ uint32_t lcnt[NSLICE];
   __shared__ uint32_t lstart[NSLICE];
   __shared__ uint32_t lcur[NSLICE];
-  __shared__ uint32_t lorder[NSLICE];   // bucket handled by lane t (by decreasing count)
+  __shared__ uint32_t lorder[NSLICE];   // bucket handled by lane group t (by decreasing count)
+#if EDC_ACC_LANES > 1
+  __shared__ __attribute__((aligned(16))) uint32_t lpart[NSLICE * EXT_WORDS];
+#endif
   const int t = threadIdx.x;
+  const int lane_b = t & (NSLICE - 1);  // bucket slot of this lane group
+  const uint32_t half = (uint32_t)t >> 8;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
   if (E == 0) return;
   const uint32_t off = offsets[bin];
   ge_p3 acc = ge_identity();
-  uint32_t my_bucket = t;
+  uint32_t my_bucket = lane_b;
   for (uint32_t c0 = 0; c0 < E; c0 += BKT_CHUNK) {
     const uint32_t ch = min((uint32_t)BKT_CHUNK, E - c0);
-    lcnt[t] = 0;
+    if (t < NSLICE) lcnt[t] = 0;
     __syncthreads();
-    for (uint32_t e = t; e < ch; e += 256) atomicAdd(&lcnt[entries[off + c0 + e].y], 1u);
+    for (uint32_t e = t; e < ch; e += ACC_THREADS) atomicAdd(&lcnt[entries[off + c0 + e].y], 1u);
     __syncthreads();
     if (t < 64) {
       uint32_t c[4], s = 0;
@@ -246,30 +265,32 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lstart[4 * t + j] = run; lcur[4 * t + j] = run; run += c[j]; }
     }
-    if (c0 == 0) {
-      // rank bucket t by (count desc, index): lanes of a wave get similar counts
-      const uint32_t mine = lcnt[t];
+    if (c0 == 0 && t >= ACC_THREADS - NSLICE) {
+      // rank bucket b by (count desc, index)
+      const int b = t - (ACC_THREADS - NSLICE);
+      const uint32_t mine = lcnt[b];
       uint32_t rank = 0;
       for (int u = 0; u < NSLICE; ++u) {
         const uint32_t o = lcnt[u];
-        rank += (o > mine) || (o == mine && u < t);
+        rank += (o > mine) || (o == mine && u < b);
       }
-      lorder[rank] = t;
+      lorder[rank] = b;
     }
     __syncthreads();
-    if (c0 == 0) my_bucket = lorder[t];
-    for (uint32_t e = t; e < ch; e += 256) {
+    if (c0 == 0) my_bucket = lorder[lane_b];
+    for (uint32_t e = t; e < ch; e += ACC_THREADS) {
       uint2 en = entries[off + c0 + e];
       uint32_t pos = atomicAdd(&lcur[en.y], 1u);
       lidx[pos] = en.x;
     }
     __syncthreads();
     const uint32_t beg = lstart[my_bucket], cnt = lcnt[my_bucket];
-    if (cnt) {
-      uint32_t e = lidx[beg];
+#if EDC_ACC_PREFETCH
+    if (half < cnt) {
+      uint32_t e = lidx[beg + half];
       ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-      for (uint32_t j = 0; j < cnt; ++j) {
-        const uint32_t e_next = (j + 1 < cnt) ? lidx[beg + j + 1] : e;
+      for (uint32_t j = half; j < cnt; j += ACC_LANES) {
+        const uint32_t e_next = (j + ACC_LANES < cnt) ? lidx[beg + j + ACC_LANES] : e;
         ge_niels q_next = ld_niels(pts, e_next & 0x7FFFFFFFu);
         if (e >> 31) q = ge_niels_neg(q);
         acc = ge_madd(acc, q);
@@ -277,8 +298,47 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum(const uint32_t* __restrict
         q = q_next;
       }
     }
+#else
+#if EDC_ACC_PROBE == 3      // measurement probe: LDS sort only, no accumulation (result wrong)
+    if (cnt > 100000) acc.X.v[0] = lidx[beg];
+#elif EDC_ACC_PROBE == 4    // measurement probe: accumulate unsorted entries straight from HBM
+    for (uint32_t j = t; j < ch; j += ACC_THREADS) {
+      const uint32_t e = entries[off + c0 + j].x;
+      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
+      if (e >> 31) q = ge_niels_neg(q);
+      acc = ge_madd(acc, q);
+    }
+#else
+    for (uint32_t j = half; j < cnt; j += ACC_LANES) {
+      const uint32_t e = lidx[beg + j];
+#endif
+#if EDC_ACC_PROBE == 3 || EDC_ACC_PROBE == 4
+    for (uint32_t j = 0; j < 0; ++j) {
+      const uint32_t e = 0;
+#endif
+#if EDC_ACC_PROBE == 1      // measurement probe: gathers + sort only (result wrong)
+      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc.X.v[k] ^= q.ypx.v[k] ^ q.ymx.v[k] ^ q.xy2d.v[k];
+#elif EDC_ACC_PROBE == 2    // measurement probe: arithmetic only, no gather (result wrong)
+      ge_niels q = ld_niels(pts, 1 + (e & 1));
+      if (e >> 31) q = ge_niels_neg(q);
+      acc = ge_madd(acc, q);
+#else
+      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
+      if (e >> 31) q = ge_niels_neg(q);
+      acc = ge_madd(acc, q);
+#endif
+    }
+#endif
     __syncthreads();
   }
+#if EDC_ACC_LANES > 1
+  if (half) st_ext(lpart + lane_b * EXT_WORDS, acc);
+  __syncthreads();
+  if (half) return;
+  acc = ge_add(acc, ld_ext(lpart + lane_b * EXT_WORDS));
+#endif
   st_ext(buckets + ((size_t)bin * NSLICE + my_bucket) * EXT_WORDS, acc);
 }
 
@@ -301,7 +361,7 @@ __global__ void __launch_bounds__(256) k_msm_reduce(const uint32_t* __restrict__
   st_ext(lpts + t * EXT_WORDS, ld_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS));
   __syncthreads();
   ge_p3 ws, tot;
-  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, lpts + (NSLICE + 64) * EXT_WORDS, ws, tot);
+  weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
   if (t < 4) {
     ge_p3 W = quad_add(ws, tot);       // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
     if (t == 0) {
@@ -322,7 +382,7 @@ __global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__
   st_ext(lpts + t * EXT_WORDS, ld_ext(slice_T + (size_t)(w * NSLICE + t) * EXT_WORDS));
   __syncthreads();
   ge_p3 ws, tot;
-  weighted_sum_256(lpts, lpts + NSLICE * EXT_WORDS, lpts + (NSLICE + 64) * EXT_WORDS, ws, tot);
+  weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
   __syncthreads();
   ge_p3 a = sum_256(ld_ext(slice_W + (size_t)(w * NSLICE + t) * EXT_WORDS), lpts);
   if (t < 4) {
@@ -429,12 +489,12 @@ void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* 
                      cursor, entries, flags);
 }
 
-static const size_t kReduceLds = (size_t)(NSLICE + 128) * EXT_WORDS * sizeof(uint32_t);  // 256 + 2 x 64 points
+static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
 
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
                        uint32_t* slice_T) {
-  hipLaunchKernelGGL(k_msm_accum, dim3(NBIN), dim3(256), 0, st, counts, offsets, entries, pts, buckets);
+  hipLaunchKernelGGL(k_msm_accum, dim3(NBIN), dim3(ACC_THREADS), 0, st, counts, offsets, entries, pts, buckets);
   hipLaunchKernelGGL(k_msm_reduce, dim3(NBIN), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
 }
 
