@@ -215,7 +215,7 @@ constexpr int BKT_CHUNK = 4096;
 #define EDC_ACC_LANES 1
 #endif
 #ifndef EDC_ACC_PREFETCH
-#define EDC_ACC_PREFETCH 1
+#define EDC_ACC_PREFETCH 0
 #endif
 #ifndef EDC_ACC_WAVES
 #define EDC_ACC_WAVES 4

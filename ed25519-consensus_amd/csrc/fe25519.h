@@ -35,6 +35,18 @@ struct fe {
 
 EDC_HD uint64_t mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
 
+// a * b + c as ONE v_mad_u64_u32 on the device. Spelled as inline asm so that LLVM cannot
+// reassociate a chain of them (it would pull the carry addend out into a separate 64-bit add).
+EDC_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c) : "vcc");
+  return d;
+#else
+  return (uint64_t)a * b + c;
+#endif
+}
+
 EDC_HD fe fe_zero() { fe r; for (int i = 0; i < 9; ++i) r.v[i] = 0; return r; }
 EDC_HD fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
 
@@ -89,57 +101,70 @@ EDC_HD fe fe_sub(const fe& a, const fe& b) {
 
 EDC_HD fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
 
-// 64-bit column sums -> reduced limbs. c[0..16] hold the schoolbook columns.
-EDC_HD fe fe_reduce_cols(uint64_t c[17]) {
-  // fold columns 9..16: 2^(29k) = 2^(29(k-9)) * 2^261, 2^261 == 1216; split each column in
-  // 32-bit halves: lo*1216 lands at k-9, hi*2^32*1216 = hi*9728 at k-8.
-#pragma unroll
-  for (int k = 9; k < 17; ++k) {
-    uint32_t lo = (uint32_t)c[k];
-    uint32_t hi = (uint32_t)(c[k] >> 32);
-    c[k - 9] += mul64(lo, 1216u);
-    c[k - 8] += mul64(hi, 9728u);
-  }
-  fe r;
-  uint64_t acc = c[0];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    r.v[i] = (uint32_t)acc & M29;
-    acc = c[i + 1] + (acc >> 29);
-  }
-  r.v[8] = (uint32_t)acc & M29;
-  uint64_t top = acc >> 29;                       // < 2^36
+// Top-column fold shared by mul and sqr: acc = the carry out of column 8 (< 2^35), i.e. the
+// value acc * 2^261 == acc * 1216 still to be added at limb 0.
+EDC_HD fe fe_fold_top(fe r, uint64_t top) {
   uint64_t t = (uint64_t)r.v[0] + mul64((uint32_t)top, 1216u) + (mul64((uint32_t)(top >> 32), 1216u) << 32);
   r.v[0] = (uint32_t)t & M29;
-  r.v[1] += (uint32_t)(t >> 29);                  // < 2^18 extra
+  r.v[1] += (uint32_t)(t >> 29);                  // < 2^17 extra
   return r;
 }
 
+// Products are accumulated column by column in ONE 64-bit register per column through chains of
+// v_mad_u64_u32 (32x32+64). Columns 9..16 (weight 2^(29k) = 2^(29(k-9)) * 2^261, 2^261 == 1216
+// mod p) are summed first; low column k then starts from the carry out of column k-1, so the
+// carry rides in a mad addend instead of a separate 64-bit add, and it absorbs the fold terms
+// lo32(col k+9) * 1216 and hi32(col k+8) * 2^32 * 1216 = hi * 9728 as two more products.
+// Column bound: 9 products < 2^60.82 (inputs < 2^30.41) + fold < 2^45.3 + carry < 2^35 < 2^64.
 EDC_HD fe fe_mul(const fe& a, const fe& b) {
-  uint64_t c[17];
+  uint64_t h[8];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) c[k] = 0;
+  for (int k = 9; k < 17; ++k) {
+    uint64_t s = 0;
 #pragma unroll
-  for (int i = 0; i < 9; ++i)
+    for (int i = k - 8; i <= 8; ++i) s += mul64(a.v[i], b.v[k - i]);
+    h[k - 9] = s;
+  }
+  fe r;
+  uint64_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) c[i + j] += mul64(a.v[i], b.v[j]);
-  return fe_reduce_cols(c);
+  for (int k = 0; k < 9; ++k) {
+    if (k < 8) acc = mad64((uint32_t)h[k], 1216u, acc);
+    if (k >= 1) acc = mad64((uint32_t)(h[k - 1] >> 32), 9728u, acc);
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc = mad64(a.v[i], b.v[k - i], acc);
+    r.v[k] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  return fe_fold_top(r, acc);
 }
 
 EDC_HD fe fe_sqr(const fe& a) {
   uint32_t d[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
-  uint64_t c[17];
+  uint64_t h[8];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) c[k] = 0;
+  for (int k = 9; k < 17; ++k) {
+    uint64_t s = 0;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    c[2 * i] += mul64(a.v[i], a.v[i]);
-#pragma unroll
-    for (int j = i + 1; j < 9; ++j) c[i + j] += mul64(a.v[i], d[j]);
+    for (int i = k - 8; 2 * i < k; ++i) s += mul64(a.v[i], d[k - i]);
+    if ((k & 1) == 0) s += mul64(a.v[k / 2], a.v[k / 2]);
+    h[k - 9] = s;
   }
-  return fe_reduce_cols(c);
+  fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    if (k < 8) acc = mad64((uint32_t)h[k], 1216u, acc);
+    if (k >= 1) acc = mad64((uint32_t)(h[k - 1] >> 32), 9728u, acc);
+#pragma unroll
+    for (int i = 0; 2 * i < k; ++i) acc = mad64(a.v[i], d[k - i], acc);
+    if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
+    r.v[k] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  return fe_fold_top(r, acc);
 }
 
 EDC_HD fe fe_sqr_n(fe a, int n) {
@@ -147,12 +172,17 @@ EDC_HD fe fe_sqr_n(fe a, int n) {
   return a;
 }
 
-// multiply by a small constant (< 2^13): stays within 64-bit columns trivially
-EDC_HD fe fe_mul_small(const fe& a, uint32_t s) {
-  uint64_t c[17];
-  for (int k = 0; k < 17; ++k) c[k] = 0;
-  for (int i = 0; i < 9; ++i) c[i] = mul64(a.v[i], s);
-  return fe_reduce_cols(c);
+// multiply by a small constant (< 2^13)
+EDC_HD fe fe_mul_small(const fe& a, uint32_t c) {
+  fe r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    acc += mul64(a.v[k], c);
+    r.v[k] = (uint32_t)acc & M29;
+    acc >>= 29;
+  }
+  return fe_fold_top(r, acc);
 }
 
 // canonical value (< p) as 9 limbs with limb 8 < 2^23

@@ -151,6 +151,38 @@ __global__ void k_fma_f32(uint64_t* out, uint32_t a, uint32_t b) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
 }
 
+
+// 32-bit two-operand ops (c = op(c, y)) and 64-bit ops used by the carry chains / SHA-512
+#define K32(NAME, ASM)                                                                 \
+  __global__ void NAME(uint64_t* out, uint32_t a, uint32_t b) {                        \
+    uint32_t c[8];                                                                     \
+    uint32_t y = b ^ blockIdx.x;                                                       \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) c[i] = a + threadIdx.x + i;          \
+    for (int it = 0; it < ITERS; ++it) {                                               \
+      _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASM : "+v"(c[i]) : "v"(y)); \
+    }                                                                                  \
+    uint32_t s = 0;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) s ^= c[i];                           \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                    \
+  }
+K32(k_alignbit, "v_alignbit_b32 %0, %0, %1, 29")
+K32(k_and_b32, "v_and_b32 %0, %0, %1")
+K32(k_bitop3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+#define K64(NAME, ASM)                                                                 \
+  __global__ void NAME(uint64_t* out, uint32_t a, uint32_t b) {                        \
+    uint64_t c[8];                                                                     \
+    uint64_t y = ((uint64_t)b << 32) ^ blockIdx.x;                                     \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) c[i] = (uint64_t)(a + threadIdx.x + i) << 20; \
+    for (int it = 0; it < ITERS; ++it) {                                               \
+      _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASM : "+v"(c[i]) : "v"(y)); \
+    }                                                                                  \
+    uint64_t s = 0;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) s ^= c[i];                           \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                    \
+  }
+K64(k_lshrrev_b64, "v_lshrrev_b64 %0, 29, %0")
+K64(k_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
+
 typedef void (*kfn)(uint64_t*, uint32_t, uint32_t);
 
 int run(const char* name, kfn f, int ops_per_iter, uint64_t* d, int blocks, int threads) {
@@ -188,6 +220,11 @@ int main() {
   run("v_mad_u64_u32", k_mad_u64_u32, 8, d, blocks, threads);
   run("mad_u64_u32+addc(pair)", k_mad_u64_u32_carry, 4, d, blocks, threads);
   run("v_fma_f64", k_fma_f64, 8, d, blocks, threads);
+  run("v_alignbit_b32", k_alignbit, 8, d, blocks, threads);
+  run("v_and_b32", k_and_b32, 8, d, blocks, threads);
+  run("v_bitop3_b32", k_bitop3, 8, d, blocks, threads);
+  run("v_lshrrev_b64", k_lshrrev_b64, 8, d, blocks, threads);
+  run("v_lshl_add_u64", k_lshl_add_u64, 8, d, blocks, threads);
   CHK(hipFree(d));
   return 0;
 }
