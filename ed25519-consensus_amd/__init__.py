@@ -39,7 +39,7 @@ ABI_SYMBOLS = [
     "edc_device_count", "edc_create", "edc_destroy", "edc_last_error", "edc_batch_verify",
     "edc_batch_verify_z", "edc_batch_verify_device", "edc_batch_partial_device", "edc_combine_partials",
     "edc_batch_submit_device", "edc_batch_wait", "edc_verify_each", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
-    "edc_sign_device", "edc_chacha_fill_device", "edc_set_timing", "edc_last_timings", "edc_timing_name",
+    "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize",
 ]
 
@@ -110,6 +110,7 @@ def load_library(path=None):
         lib.edc_sign.argtypes = [c_vp, c_sz, c_u8p, c_sz, c_vp, c_u8p, c_u64p, c_vp, c_vp]
         lib.edc_sign_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]
         lib.edc_chacha_fill_device.argtypes = [c_vp, c_u8p, ctypes.c_uint64, ctypes.c_uint64, c_vp]
+        lib.edc_reserve.argtypes = [c_vp, c_sz]
         lib.edc_set_timing.argtypes = [c_vp, ctypes.c_int]
         lib.edc_last_timings.restype = ctypes.c_int
         lib.edc_last_timings.argtypes = [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]

@@ -13,7 +13,7 @@ namespace {
 
 // phases in enqueue order (each bracketed by HIP events on the slot stream)
 enum Phase { PH_CHALLENGE, PH_KEYS, PH_DECOMP, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
-const char* kPhaseNames[PH_N] = {"challenge_sha512", "keys_group", "decompress_R_and_keys",
+const char* kPhaseNames[PH_N] = {"challenge_sha512", "keys_group", "decompress_R",
                                  "coef_chacha_scalar", "msm_bin", "msm_bucket", "msm_window_final"};
 
 template <typename T>
@@ -30,6 +30,8 @@ constexpr int kSlots = 2;  // batches that can be in flight per context
 // One in-flight batch: its own HIP stream and every per-batch device buffer.
 struct Slot {
   hipStream_t st = nullptr;
+  hipStream_t side = nullptr;   // key decoding (+ few-key shifts), concurrent with R decoding
+  hipEvent_t fork = nullptr, join = nullptr;
   size_t cap_n = 0, cap_T = 0;
   uint32_t *k = nullptr, *key_slot = nullptr, *key_index = nullptr, *key_rep = nullptr;
   uint32_t *table = nullptr, *slot_key = nullptr;
@@ -51,7 +53,7 @@ struct Slot {
 struct edc_ctx {
   int device = 0;
   std::string err;
-  uint32_t* btab = nullptr;     // [1..8]B affine Niels
+  uint32_t* btab = nullptr;     // [1..8]B and [2^128]B, affine Niels
   Slot slot[kSlots];
   // staging for the host-pointer entry points (used on slot 0's stream)
   size_t cap_n = 0, cap_msg = 0, cap_aux = 0;
@@ -98,6 +100,9 @@ static size_t next_pow2(size_t x) {
 static int init_slot(edc_ctx* ctx, Slot& s) {
   if (s.st) return 0;
   CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking));
+  CK(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
   CK(dalloc(&s.flags, FLAG_COUNT));
   CK(dalloc(&s.d_out, 256));
   CK(hipHostMalloc((void**)&s.h_out, 256));
@@ -119,8 +124,8 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.key_rep, cap));
   CK(dalloc(&s.table, T));
   CK(dalloc(&s.slot_key, T));
-  CK(dalloc(&s.pts, (1 + 2 * cap) * NIELS_WORDS));
-  CK(dalloc(&s.scal, (1 + 2 * cap) * 8));
+  CK(dalloc(&s.pts, (2 + 2 * cap) * NIELS_WORDS));   // >= msm_num_points(n, m) for any m <= n
+  CK(dalloc(&s.scal, (2 + 2 * cap) * 8));
   CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
   CK(dalloc(&s.u_acc, KEY_ACC_LIMBS));
   CK(dalloc(&s.counts, NBIN));
@@ -245,16 +250,23 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   mark(PH_KEYS);
   launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
               s.pts, s.key_acc, s.flags);
+  // fork: distinct keys are decoded (and, few-key mode, shifted by 2^128) on the side stream
+  // while the main stream decodes the R_i; joined before the bucket accumulation reads them
+  CK(hipEventRecord(s.fork, st));
+  CK(hipStreamWaitEvent(s.side, s.fork, 0));
+  launch_key_points(s.side, N, d_vk, s.key_rep, s.pts, ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags);
+  CK(hipEventRecord(s.join, s.side));
   mark(PH_DECOMP);
-  launch_decompress(st, N, d_sig, d_vk, s.key_rep, s.pts, s.flags);
+  launch_decompress(st, N, d_sig, s.pts, s.flags);
   mark(PH_COEF);
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags);
   mark(PH_MSM_BIN);
   launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  CK(hipStreamWaitEvent(st, s.join, 0));
   mark(PH_MSM_BUCKET);
   launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.pts, s.buckets, s.slice_W, s.slice_T);
   mark(PH_MSM_TAIL);
-  launch_msm_tail(st, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
+  launch_msm_tail(st, s.counts, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
   mark(PH_N);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, st));
@@ -305,7 +317,7 @@ edc_ctx* edc_create(int device) {
   edc_ctx* ctx = new edc_ctx();
   ctx->device = device;
   bool ok = hipSetDevice(device) == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
-            dalloc(&ctx->btab, 8 * NIELS_WORDS) == hipSuccess;
+            dalloc(&ctx->btab, BTAB_ENTRIES * NIELS_WORDS) == hipSuccess;
   if (ok) {
     launch_init_btable(ctx->st(), ctx->btab);
     ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->st()) == hipSuccess;
@@ -328,6 +340,10 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
+    if (s.side) (void)hipStreamSynchronize(s.side);
+    if (s.fork) (void)hipEventDestroy(s.fork);
+    if (s.join) (void)hipEventDestroy(s.join);
+    if (s.side) (void)hipStreamDestroy(s.side);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->aux, ctx->btab};
@@ -533,6 +549,17 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
   launch_chacha_fill(ctx->st(), k, blk0, nblocks, reinterpret_cast<uint32_t*>(d_out));
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->st()));
+  return 0;
+}
+
+int edc_reserve(edc_ctx* ctx, size_t n) {
+  if (!ctx) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  for (Slot& s : ctx->slot) {
+    if (s.pending) { ctx->err = "reserve with a batch in flight"; return EDC_ERR_ARG; }
+    int rc = ensure_slot(ctx, s, n);
+    if (rc) return rc;
+  }
   return 0;
 }
 

@@ -88,7 +88,29 @@ __device__ __forceinline__ int scalar_digit(const uint32_t s[8], int w, int& car
 // 64-bit limb-sum accumulators per distinct key (12 limbs of a 128 x 256-bit product)
 constexpr int KEY_ACC_LIMBS = 12;
 
-// flags slot indices
-enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_COUNT = 8 };
+// flags slot indices (FLAG_WINMASK: bit w set when MSM window w has at least one entry)
+enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_WINMASK = 3, FLAG_COUNT = 8 };
+
+// Few-key batches (consensus votes: m validators << n votes). Every full-width coefficient
+// (B and each distinct key) is split as c = c_lo + 2^128 c_hi over the points P and
+// [2^128]P, so EVERY scalar of the MSM is < 2^128 and only the 8 low windows exist: half the
+// bucket reductions and half the Horner doublings. The shifted key points cost 128 doublings
+// per key, computed on a side stream under the R decompression; [2^128]B is a context
+// constant. Point layout in few-key mode:
+//   0 = B, 1..n = R_i, n+1..n+m = A_j, n+m+1..n+2m = [2^128]A_j, n+2m+1 = [2^128]B.
+constexpr uint32_t FEW_KEY_MIN_N = 4096;
+constexpr int BTAB_BSHIFT = 8;     // context table entry holding [2^128]B
+constexpr int BTAB_ENTRIES = 9;
+constexpr uint32_t FEW_KEY_RATIO = 16;
+__host__ __device__ __forceinline__ bool few_key_mode(uint32_t n, uint32_t m) {
+  return n >= FEW_KEY_MIN_N && (uint64_t)m * FEW_KEY_RATIO <= n;
+}
+__host__ __device__ __forceinline__ uint32_t msm_num_points(uint32_t n, uint32_t m) {
+  return few_key_mode(n, m) ? n + 2 * m + 2 : 1 + n + m;
+}
+// point p of the MSM carries a scalar < 2^128 (8 windows, top digit unsigned)?
+__device__ __forceinline__ bool msm_short_scalar(uint32_t p, uint32_t n, bool few) {
+  return few || (p >= 1 && p <= n);
+}
 
 }  // namespace edc

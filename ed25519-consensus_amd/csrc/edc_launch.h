@@ -7,8 +7,9 @@ namespace edc {
 // edc_prep.hip
 void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
-void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
-                       uint32_t* pts, int* flags);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
+void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
+                       const uint32_t* bshift, int* flags);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
                  uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
@@ -23,8 +24,8 @@ void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* o
                        const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
                        uint32_t* slice_T);
 size_t msm_bucket_words();
-void launch_msm_tail(hipStream_t st, const uint32_t* slice_W, const uint32_t* slice_T, uint32_t* win,
-                     const int* flags, int want_compress, uint8_t* out);
+void launch_msm_tail(hipStream_t st, const uint32_t* counts, const uint32_t* slice_W, const uint32_t* slice_T,
+                     uint32_t* win, int* flags, int want_compress, uint8_t* out);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
                     uint8_t* out);
 size_t msm_entry_capacity(uint32_t n);

@@ -4,7 +4,9 @@
 // yields the same group element).
 //
 // Points p: 0 = B, 1..n = R_i (128-bit z, 8 windows, top digit unsigned up to 2^16),
-//           n+1..n+m = distinct keys (253-bit, 16 signed windows).
+//           n+1..n+m = distinct keys (253-bit, 16 signed windows); in few-key mode
+//           (edc_common.h) B and the keys carry 128-bit halves and their [2^128] twins follow,
+//           so every point has 8 windows.
 // Buckets: signed radix-2^16 digits d, bucket |d| in window w. A bin = (window, slice of 256
 // consecutive buckets) = one workgroup. Entries are binned by a count / scan / scatter pass
 // (LDS-aggregated histograms, no global sort), then each bin's workgroup counting-sorts its
@@ -31,14 +33,16 @@ __global__ void __launch_bounds__(256) k_msm_count(uint32_t n, const uint32_t* _
   __shared__ uint32_t hist[NBIN];
   for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  const uint32_t npts = 1 + n + (uint32_t)flags[FLAG_NKEYS];
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  const bool few = few_key_mode(n, m);
+  const uint32_t npts = msm_num_points(n, m);
   const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
   for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
     uint32_t p = p0 + t;
     if (p >= npts) break;
     uint32_t s[8];
     load_scalar(scal, p, s);
-    const bool isR = p >= 1 && p <= n;
+    const bool isR = msm_short_scalar(p, n, few);
     const int nwin = isR ? NWIN_Z : NWIN_FULL;
     int carry = 0;
     for (int w = 0; w < nwin; ++w) {
@@ -88,7 +92,9 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
   __shared__ uint32_t gbase[NBIN];
   for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  const uint32_t npts = 1 + n + (uint32_t)flags[FLAG_NKEYS];
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  const bool few = few_key_mode(n, m);
+  const uint32_t npts = msm_num_points(n, m);
   const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
   // pass 1: local ranks (recomputed in pass 2 from the same digits)
   for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
@@ -96,7 +102,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
     if (p >= npts) break;
     uint32_t s[8];
     load_scalar(scal, p, s);
-    const bool isR = p >= 1 && p <= n;
+    const bool isR = msm_short_scalar(p, n, few);
     const int nwin = isR ? NWIN_Z : NWIN_FULL;
     int carry = 0;
     for (int w = 0; w < nwin; ++w) {
@@ -119,7 +125,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t*
     if (p >= npts) break;
     uint32_t s[8];
     load_scalar(scal, p, s);
-    const bool isR = p >= 1 && p <= n;
+    const bool isR = msm_short_scalar(p, n, few);
     const int nwin = isR ? NWIN_Z : NWIN_FULL;
     int carry = 0;
     for (int w = 0; w < nwin; ++w) {
@@ -372,12 +378,17 @@ __global__ void __launch_bounds__(256) k_msm_reduce(const uint32_t* __restrict__
 }
 
 // one workgroup per window: Win_w = sum_s W_s + 256 * sum_s s T_s
-__global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__ slice_W,
+// (a window without entries -- windows 8..15 in few-key mode -- is skipped; FLAG_WINMASK records
+// the non-empty ones for the Horner pass)
+__global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ slice_W,
                                                     const uint32_t* __restrict__ slice_T,
-                                                    uint32_t* __restrict__ win) {
+                                                    uint32_t* __restrict__ win, int* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int t = threadIdx.x;
   const uint32_t w = blockIdx.x;
+  if (!__syncthreads_or(counts[w * NSLICE + t] != 0)) return;
+  if (t == 0) atomicOr(&flags[FLAG_WINMASK], 1 << w);
   uint32_t* lpts = smem;
   st_ext(lpts + t * EXT_WORDS, ld_ext(slice_T + (size_t)(w * NSLICE + t) * EXT_WORDS));
   __syncthreads();
@@ -447,10 +458,14 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
 __global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restrict__ flags,
                             int want_compress, uint8_t* __restrict__ out) {
   if (threadIdx.x >= 4 || blockIdx.x != 0) return;
-  ge_p3 acc = ld_ext(win + (size_t)(NWIN_FULL - 1) * EXT_WORDS);
-  for (int w = NWIN_FULL - 2; w >= 0; --w) {
-    for (int k = 0; k < WIN_BITS; ++k) acc = quad_dbl(acc);
-    acc = quad_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
+  // Horner from the highest non-empty window (windows without entries were never written)
+  const uint32_t mask = (uint32_t)flags[FLAG_WINMASK];
+  const int top = mask ? 31 - __builtin_clz(mask) : -1;
+  ge_p3 acc = ge_identity();
+  for (int w = top; w >= 0; --w) {
+    if (w != top)
+      for (int k = 0; k < WIN_BITS; ++k) acc = quad_dbl(acc);
+    if (mask & (1u << w)) acc = quad_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
   }
   ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
   if (threadIdx.x != 0) return;
@@ -500,9 +515,9 @@ void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* o
 
 size_t msm_bucket_words() { return (size_t)NBIN * NSLICE * EXT_WORDS; }
 
-void launch_msm_tail(hipStream_t st, const uint32_t* slice_W, const uint32_t* slice_T, uint32_t* win,
-                     const int* flags, int want_compress, uint8_t* out) {
-  hipLaunchKernelGGL(k_msm_window, dim3(NWIN_FULL), dim3(256), kReduceLds, st, slice_W, slice_T, win);
+void launch_msm_tail(hipStream_t st, const uint32_t* counts, const uint32_t* slice_W, const uint32_t* slice_T,
+                     uint32_t* win, int* flags, int want_compress, uint8_t* out) {
+  hipLaunchKernelGGL(k_msm_window, dim3(NWIN_FULL), dim3(256), kReduceLds, st, counts, slice_W, slice_T, win, flags);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, win, flags, want_compress, out);
 }
 

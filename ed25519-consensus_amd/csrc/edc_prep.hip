@@ -10,6 +10,7 @@
 //   k_key_final     A_coeff = sum v_i mod l per key; B_coeff = -sum u_i mod l
 #include "edc_common.h"
 #include "edc_launch.h"
+#include "ge_quad.h"
 
 namespace edc {
 
@@ -30,28 +31,66 @@ __global__ void __launch_bounds__(256, 4) k_challenge(uint32_t n, const uint8_t*
   kp[1] = make_uint4(k.v[4], k.v[5], k.v[6], k.v[7]);
 }
 
-// One launch decodes both the signatures' R_i (threads [0, n) -> points[1 + i]) and the distinct
-// keys (threads [n, n + m) -> points[1 + n + j]), so the few-key case (m = 150 validators) rides
-// along with the R decodes instead of paying a serial single-wave launch of its own.
+// ZIP215 decode of every signature's R_i -> points[1 + i] (affine Niels).
 __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
-                                                       const uint8_t* __restrict__ vk,
-                                                       const uint32_t* __restrict__ key_rep,
                                                        uint32_t* __restrict__ pts, int* __restrict__ flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint8_t* enc;
-  if (i < n) {
-    enc = sig + (size_t)i * 64;
-  } else {
-    const uint32_t j = i - n;
-    if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
-    enc = vk + (size_t)key_rep[j] * 32;
-  }
+  if (i >= n) return;
   uint32_t w[8];
-  ld_words8(enc, w);
+  ld_words8(sig + (size_t)i * 64, w);
   ge_p3 P;
   const bool ok = ge_decompress(w, P);
   st_niels(pts, 1 + i, ge_to_niels_affine(P));
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
+}
+
+// Side stream, concurrent with k_decompress: ZIP215 decode of each distinct key j (its first
+// signature's raw bytes, src/batch.rs:183-185) -> points[1 + n + j].
+__global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t* __restrict__ vk,
+                                                       const uint32_t* __restrict__ key_rep,
+                                                       uint32_t* __restrict__ pts, int* __restrict__ flags) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
+  uint32_t w[8];
+  ld_words8(vk + (size_t)key_rep[j] * 32, w);
+  ge_p3 P;
+  const bool ok = ge_decompress(w, P);
+  st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
+  if (!ok) atomicOr(&flags[FLAG_BAD], 1);
+}
+
+// 1/2 mod p: affine (x, y) back from a Niels record, x = (ypx - ymx)/2, y = (ypx + ymx)/2
+__device__ __forceinline__ fe fe_inv2() {
+  return fe_const(0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                  0xffffffffu, 0x3fffffffu);
+}
+
+// Few-key mode only (side stream, after k_key_points): [2^128]A_j as affine Niels at
+// points[1 + n + m + j], one quad of lanes per key (quad-cooperative doublings, ge_quad.h), and
+// the context constant [2^128]B copied to points[n + 2m + 1].
+__global__ void __launch_bounds__(64) k_key_shift(uint32_t n, uint32_t* __restrict__ pts,
+                                                  const uint32_t* __restrict__ bshift,
+                                                  const int* __restrict__ flags) {
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  if (!few_key_mode(n, m)) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < NIELS_WORDS) pts[(size_t)(n + 2 * m + 1) * NIELS_WORDS + t] = bshift[t];
+  const uint32_t j = t >> 2;          // whole quads share j: a quad is active or exits together
+  if (j >= m) return;
+  const ge_niels a = ld_niels(pts, 1 + n + j);
+  ge_p3 P;
+  P.X = fe_mul(fe_sub(a.ypx, a.ymx), fe_inv2());
+  P.Y = fe_mul(fe_add(a.ypx, a.ymx), fe_inv2());
+  P.Z = fe_one();
+  P.T = fe_mul(P.X, P.Y);
+  for (int k = 0; k < 128; ++k) P = quad_dbl(P);
+  const fe zi = fe_invert(P.Z);       // every lane of the quad holds the same point
+  ge_p3 Q;
+  Q.X = fe_mul(P.X, zi);
+  Q.Y = fe_mul(P.Y, zi);
+  Q.Z = fe_one();
+  Q.T = fe_mul(Q.X, Q.Y);
+  if ((t & 3) == 0) st_niels(pts, 1 + n + m + j, ge_to_niels_affine(Q));
 }
 
 __device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t salt) {
@@ -265,22 +304,34 @@ __device__ __forceinline__ sc reduce_limb_sums(const unsigned long long* L) {
   return sc_reduce_wide(x);
 }
 
+// coefficient c of point p; in few-key mode c_lo goes to p and c_hi to its [2^128]-shifted twin
+__device__ __forceinline__ void store_coeff(uint32_t* scal, uint32_t p, uint32_t p_shift, const sc& c, bool few) {
+  uint4* d = reinterpret_cast<uint4*>(scal + (size_t)p * 8);
+  d[0] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
+  if (few) {
+    d[1] = make_uint4(0, 0, 0, 0);
+    uint4* h = reinterpret_cast<uint4*>(scal + (size_t)p_shift * 8);
+    h[0] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
+    h[1] = make_uint4(0, 0, 0, 0);
+  } else {
+    d[1] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned long long* __restrict__ key_acc,
                                                    const unsigned long long* __restrict__ u_acc,
                                                    uint32_t* __restrict__ scal,
                                                    const int* __restrict__ flags) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  const bool few = few_key_mode(n, m);
   if (j < m) {
     sc a = reduce_limb_sums(key_acc + (size_t)j * PL);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) scal[(size_t)(1 + n + j) * 8 + q] = a.v[q];
+    store_coeff(scal, 1 + n + j, n + m + 1 + j, a, few);
   }
   if (j == 0) {
     sc u = reduce_limb_sums(u_acc);
-    sc b = sc_sub(sc_zero(), u);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) scal[q] = b.v[q];
+    store_coeff(scal, 0, n + 2 * m + 1, sc_sub(sc_zero(), u), few);
   }
 }
 
@@ -295,10 +346,18 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k) {
   if (n) hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, sig, msg, off, k);
 }
-void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
-                       uint32_t* pts, int* flags) {
-  // grid covers n R points + up to n distinct keys (m is read on the device)
-  if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(2ull * n, 256)), dim3(256), 0, st, n, sig, vk, key_rep, pts, flags);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags) {
+  if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
+}
+void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
+                       const uint32_t* bshift, int* flags) {
+  if (!n) return;
+  // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
+  // on the device and surplus blocks exit at once
+  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags);
+  if (n >= FEW_KEY_MIN_N)
+    hipLaunchKernelGGL(k_key_shift, dim3(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64)), dim3(64), 0, st, n,
+                       pts, bshift, flags);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,

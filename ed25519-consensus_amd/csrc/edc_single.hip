@@ -10,19 +10,26 @@
 
 namespace edc {
 
-// [i]B for i = 1..8 as affine Niels, filled once per context
+__device__ __forceinline__ ge_niels to_niels(const ge_p3& P) {  // x = X/Z, y = Y/Z
+  fe zi = fe_invert(P.Z);
+  ge_p3 a;
+  a.X = fe_mul(P.X, zi); a.Y = fe_mul(P.Y, zi); a.Z = fe_one(); a.T = fe_mul(a.X, a.Y);
+  return ge_to_niels_affine(a);
+}
+
+// context constants as affine Niels: [i]B for i = 1..8 (entries 0..7) and [2^128]B (entry
+// BTAB_BSHIFT, the few-key MSM's shifted basepoint)
 __global__ void k_init_btable(uint32_t* btab) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ge_p3 B = ge_basepoint();
   ge_p3 acc = B;
   for (int i = 0; i < 8; ++i) {
-    // to affine: x = X/Z, y = Y/Z
-    fe zi = fe_invert(acc.Z);
-    ge_p3 a;
-    a.X = fe_mul(acc.X, zi); a.Y = fe_mul(acc.Y, zi); a.Z = fe_one(); a.T = fe_mul(a.X, a.Y);
-    st_niels(btab, i, ge_to_niels_affine(a));
+    st_niels(btab, i, to_niels(acc));
     acc = ge_add(acc, B);
   }
+  acc = B;
+  for (int k = 0; k < 128; ++k) acc = ge_dbl(acc);
+  st_niels(btab, BTAB_BSHIFT, to_niels(acc));
 }
 
 // signed radix-16 digits of a scalar < 2^255, 64 digits in [-7, 8]

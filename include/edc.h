@@ -153,6 +153,12 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
                            uint8_t* d_out);
 
 /*
+ * Pre-allocate the workspaces of every in-flight slot for batches of up to n items (otherwise
+ * they grow on first use). Not a reference API: a setup call for streaming callers.
+ */
+int edc_reserve(edc_ctx* ctx, size_t n);
+
+/*
  * Per-phase device timings of the last batch call (HIP events on the context stream), enabled
  * by edc_set_timing(ctx, 1). Returns the number of phases written (<= cap); names via
  * edc_timing_name(i).
