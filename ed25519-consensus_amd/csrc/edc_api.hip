@@ -39,8 +39,10 @@ struct Slot {
   unsigned long long *key_acc = nullptr, *u_acc = nullptr;
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr;
   uint2* entries = nullptr;
+  uint32_t* sorted = nullptr;   // entries' point indices sorted by bucket within each bin
   uint32_t *slice_W = nullptr, *slice_T = nullptr, *win = nullptr;
   uint32_t* buckets = nullptr;  // NBIN x 256 bucket sums (extended), fixed size
+  uint32_t* heads = nullptr;    // NBIN x 256 head partials of the segmented accumulation
   int* flags = nullptr;
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
@@ -80,14 +82,15 @@ struct edc_ctx {
 
 static void free_slot_buffers(Slot& s) {
   void* ptrs[] = {s.k, s.key_slot, s.key_index, s.key_rep, s.table, s.slot_key, s.pts, s.scal, s.key_acc,
-                  s.u_acc, s.counts, s.offsets, s.cursor, s.entries, s.slice_W, s.slice_T, s.win, s.buckets};
+                  s.u_acc, s.counts, s.offsets, s.cursor, s.entries, s.sorted, s.slice_W, s.slice_T, s.win, s.buckets, s.heads};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s.k = s.key_slot = s.key_index = s.key_rep = s.table = s.slot_key = s.pts = s.scal = nullptr;
   s.key_acc = s.u_acc = nullptr;
   s.counts = s.offsets = s.cursor = nullptr;
   s.entries = nullptr;
-  s.slice_W = s.slice_T = s.win = s.buckets = nullptr;
+  s.sorted = nullptr;
+  s.slice_W = s.slice_T = s.win = s.buckets = s.heads = nullptr;
   s.cap_n = s.cap_T = 0;
 }
 
@@ -132,10 +135,12 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.offsets, NBIN));
   CK(dalloc(&s.cursor, NBIN));
   CK(dalloc(&s.entries, msm_entry_capacity((uint32_t)cap)));
+  CK(dalloc(&s.sorted, msm_entry_capacity((uint32_t)cap)));
   CK(dalloc(&s.slice_W, (size_t)NBIN * EXT_WORDS));
   CK(dalloc(&s.slice_T, (size_t)NBIN * EXT_WORDS));
   CK(dalloc(&s.win, (size_t)NWIN_FULL * EXT_WORDS));
   CK(dalloc(&s.buckets, msm_bucket_words()));
+  CK(dalloc(&s.heads, msm_bucket_words()));
   launch_init_basepoint(s.st, s.pts);
   CK(hipGetLastError());
   s.cap_n = cap;
@@ -264,7 +269,7 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
   CK(hipStreamWaitEvent(st, s.join, 0));
   mark(PH_MSM_BUCKET);
-  launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.pts, s.buckets, s.slice_W, s.slice_T);
+  launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
   mark(PH_MSM_TAIL);
   launch_msm_tail(st, s.counts, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
   mark(PH_N);

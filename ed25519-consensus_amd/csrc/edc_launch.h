@@ -21,8 +21,8 @@ void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
-                       uint32_t* slice_T);
+                       const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
+                       uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T);
 size_t msm_bucket_words();
 void launch_msm_tail(hipStream_t st, const uint32_t* counts, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out);

@@ -348,6 +348,166 @@ __global__ void __launch_bounds__(ACC_THREADS, EDC_ACC_WAVES) k_msm_accum(const 
   st_ext(buckets + ((size_t)bin * NSLICE + my_bucket) * EXT_WORDS, acc);
 }
 
+#ifndef EDC_ACC_DMA
+#define EDC_ACC_DMA 1
+#endif
+
+// ---- bucket accumulation with coalesced row gathers (EDC_ACC_DMA) ----
+// One workgroup per bin, one lane per bucket (buckets handed to lanes by decreasing entry count,
+// so the lanes of a wave run about the same number of rounds). The bin's entries are counting-
+// sorted by bucket through LDS counters into `sorted` (global, so a bin of any size is sorted in
+// one pass and LDS stays free for the row buffers). Each round, every wave gathers the next Niels
+// record of each of its 64 lanes with 7 LDS-DMA wave-instructions (global_load_lds_dwordx4):
+// instruction k moves pieces 64k..64k+63 of the wave's 64 x 7 sixteen-byte pieces, i.e. whole
+// 112-byte rows, 9-10 rows per instruction, instead of 64 scattered 16-byte pieces per load
+// instruction as a row-per-lane register gather issues. Rows land row-major (112-byte stride:
+// 28 words, odd multiple of 4 banks, so the row reads are conflict-free) and each lane reads its
+// own row back.
+constexpr int ROW_PIECES = 7;                        // 16-byte pieces of a record carrying data
+constexpr int ROW_WORDS = ROW_PIECES * 4;            // 28
+constexpr int WAVE_ROWS_WORDS = 64 * ROW_WORDS;      // 7 KB of LDS per wave
+
+__device__ __forceinline__ void dma_piece(const uint32_t* gsrc, uint32_t* lds_wave_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ ge_niels ld_row_lds(const uint32_t* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint32_t w[28];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    uint4 t = q[i];
+    w[4 * i] = t.x; w[4 * i + 1] = t.y; w[4 * i + 2] = t.z; w[4 * i + 3] = t.w;
+  }
+  ge_niels n;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) { n.ypx.v[i] = w[i]; n.ymx.v[i] = w[9 + i]; n.xy2d.v[i] = w[18 + i]; }
+  return n;
+}
+
+// Lane balance (segmented accumulation): lane t takes the sorted positions [E t/256, E (t+1)/256)
+// of its bin, so every lane runs the same number of rounds whatever the Poisson spread of the
+// bucket sizes (one bucket per lane ran each workgroup as long as its largest bucket). A lane
+// flushes its running sum whenever its positions cross a bucket end: a bucket that starts and
+// ends inside the lane's range is stored whole; the partial of a bucket that began before the
+// range ("head") goes to the lane's scratch slot; the lane holding a bucket's first entry adds the
+// heads of the following lanes the bucket covers after a barrier and stores the bucket.
+__device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin, uint32_t b) {
+  return buckets + ((size_t)bin * NSLICE + b) * EXT_WORDS;
+}
+
+__global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint32_t* __restrict__ counts,
+                                                                   const uint32_t* __restrict__ offsets,
+                                                                   const uint2* __restrict__ entries,
+                                                                   uint32_t* __restrict__ sorted,
+                                                                   const uint32_t* __restrict__ pts,
+                                                                   uint32_t* __restrict__ buckets,
+                                                                   uint32_t* __restrict__ heads) {
+  __shared__ uint32_t lcnt[NSLICE];
+  __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
+  __shared__ uint32_t lcur[NSLICE];
+  __shared__ __attribute__((aligned(16))) uint32_t lrows[4][WAVE_ROWS_WORDS];
+  const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  const uint32_t bin = blockIdx.x;
+  const uint32_t E = counts[bin];
+  if (E == 0) return;
+  const uint32_t off = offsets[bin];
+  lcnt[t] = 0;
+  __syncthreads();
+  for (uint32_t e = t; e < E; e += 256) atomicAdd(&lcnt[entries[off + e].y], 1u);
+  __syncthreads();
+  if (t < 64) {
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c[q] = lcnt[4 * t + q]; sum += c[q]; }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t v = __shfl_up(incl, d, 64);
+      if (t >= d) incl += v;
+    }
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { lcur[4 * t + q] = run; run += c[q]; lend[4 * t + q] = run; }
+  }
+  __syncthreads();
+  if (lcnt[t] == 0) st_ext(bucket_slot(buckets, bin, t), ge_identity());
+  for (uint32_t e = t; e < E; e += 256) {
+    const uint2 en = entries[off + e];
+    sorted[off + atomicAdd(&lcur[en.y], 1u)] = en.x;
+  }
+  __syncthreads();   // workgroup-scope release/acquire: the sorted lists are read back below
+  const uint32_t lo = (uint32_t)(((uint64_t)E * t) >> 8), hi = (uint32_t)(((uint64_t)E * (t + 1)) >> 8);
+  // bucket holding position lo: the first b with lend[b] > lo
+  uint32_t cb = 0;
+#pragma unroll
+  for (int step = 128; step >= 1; step >>= 1)
+    if (lend[cb + step - 1] <= lo) cb += step;
+  cb = min(cb, (uint32_t)NSLICE - 1);              // lanes with an empty range (E < 256)
+  const bool head0 = lo < hi && lend[cb] - lcnt[cb] < lo;   // first bucket began in an earlier lane
+  bool in_head = head0;
+  uint32_t cend = lend[cb];
+  const uint32_t rounds = __builtin_amdgcn_readfirstlane(((uint64_t)E + 255) >> 8);
+  uint32_t* wrows = lrows[wv];
+  uint32_t* my_head = heads + ((size_t)bin * NSLICE + t) * EXT_WORDS;
+  ge_p3 acc = ge_identity();
+  uint32_t e_next = lo < hi ? sorted[off + lo] : 0u;
+  for (uint32_t j = 0; j < rounds; ++j) {
+    const uint32_t pos = lo + j;
+    if (pos < hi && pos == cend) {                 // the running bucket ended: flush it
+      st_ext(in_head ? my_head : bucket_slot(buckets, bin, cb), acc);
+      acc = ge_identity();
+      in_head = false;
+      do { ++cb; } while (lend[cb] <= pos);        // skip empty buckets
+      cend = lend[cb];
+    }
+    const uint32_t e = e_next;
+    if (pos + 1 < hi) e_next = sorted[off + pos + 1];
+    const uint32_t row = e & 0x7FFFFFFFu;          // lanes past their range re-read a valid row
+#if EDC_ACC_PROBE == 2      // measurement probe: arithmetic only, no gather (result wrong)
+    ge_niels q = ld_niels(pts, 1 + (row & 1));
+#else
+    uint32_t lane_o = (uint32_t)lane;
+    asm volatile("" : "+v"(lane_o));               // recompute the piece map each round: hoisted
+#pragma unroll                                     // out of the loop it costs 14 live VGPRs
+    for (int k = 0; k < ROW_PIECES; ++k) {
+      const uint32_t g = 64u * k + lane_o;
+      const uint32_t src = g / 7u, piece = g - 7u * src;
+      const uint32_t r = (uint32_t)__shfl((int)row, (int)src, 64);
+      dma_piece(pts + (size_t)r * NIELS_WORDS + piece * 4, wrows + k * 256);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): this round's rows are in LDS
+    ge_niels q = ld_row_lds(wrows + lane * ROW_WORDS);
+#endif
+    if (pos < hi) {
+#if EDC_ACC_PROBE == 1      // measurement probe: gathers only (result wrong)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc.X.v[k] ^= q.ypx.v[k] ^ q.ymx.v[k] ^ q.xy2d.v[k];
+#else
+      if (e >> 31) q = ge_niels_neg(q);
+      acc = ge_madd(acc, q);
+#endif
+    }
+  }
+  // the open segment: a head partial, a whole bucket ending at hi, or the first part of a bucket
+  // that continues into the next lanes
+  const bool owns_open = lo < hi && !in_head;
+  const bool continues = owns_open && cend > hi;
+  if (lo < hi && in_head) st_ext(my_head, acc);
+  if (owns_open && !continues) st_ext(bucket_slot(buckets, bin, cb), acc);
+  __syncthreads();   // heads visible to the owners
+  if (continues) {
+    for (uint32_t u = t + 1; u < NSLICE; ++u) {
+      const uint32_t lo_u = (uint32_t)(((uint64_t)E * u) >> 8), hi_u = (uint32_t)(((uint64_t)E * (u + 1)) >> 8);
+      if (lo_u < hi_u) acc = ge_add(acc, ld_ext(heads + ((size_t)bin * NSLICE + u) * EXT_WORDS));  // lanes
+      if (cend <= hi_u) break;                     // with an empty range (E < 256) hold no head
+    }
+    st_ext(bucket_slot(buckets, bin, cb), acc);
+  }
+}
+
 // one workgroup per bin: W_s = sum_t (t+1) S_t and T_s = sum_t S_t (quad-cooperative)
 __global__ void __launch_bounds__(256) k_msm_reduce(const uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ buckets,
@@ -507,9 +667,16 @@ void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
 
 void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, const uint32_t* pts, uint32_t* buckets, uint32_t* slice_W,
-                       uint32_t* slice_T) {
+                       const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
+                       uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
+#if EDC_ACC_DMA
+  hipLaunchKernelGGL(k_msm_accum_dma, dim3(NBIN), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
+                     heads);
+#else
+  (void)sorted;
+  (void)heads;
   hipLaunchKernelGGL(k_msm_accum, dim3(NBIN), dim3(ACC_THREADS), 0, st, counts, offsets, entries, pts, buckets);
+#endif
   hipLaunchKernelGGL(k_msm_reduce, dim3(NBIN), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
 }
 

@@ -88,15 +88,33 @@ EDC_HD ge_p3 ge_neg(const ge_p3& P) {
   ge_p3 r; r.X = fe_neg(P.X); r.Y = P.Y; r.Z = P.Z; r.T = fe_neg(P.T); return r;
 }
 
+// Scheduling fence between the multiplications of a point formula on the device: the seven
+// products of a mixed addition are independent, and interleaving them lets the scheduler keep
+// several 17-column accumulators live at once, which spills at 4 waves/SIMD (128 VGPRs).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define EDC_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define EDC_SCHED_FENCE() ((void)0)
+#endif
+
 // P + Q, Q affine Niels: 7M
 EDC_HD ge_p3 ge_madd(const ge_p3& P, const ge_niels& q) {
   fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  EDC_SCHED_FENCE();
   fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
+  EDC_SCHED_FENCE();
   fe C = fe_mul(P.T, q.xy2d);
+  EDC_SCHED_FENCE();
   fe D = fe_add_c(P.Z, P.Z);
   fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
   ge_p3 r;
-  r.X = fe_mul(E, F); r.Y = fe_mul(G, H); r.T = fe_mul(E, H); r.Z = fe_mul(F, G);
+  r.X = fe_mul(E, F);
+  EDC_SCHED_FENCE();
+  r.Y = fe_mul(G, H);
+  EDC_SCHED_FENCE();
+  r.T = fe_mul(E, H);
+  EDC_SCHED_FENCE();
+  r.Z = fe_mul(F, G);
   return r;
 }
 
@@ -140,9 +158,11 @@ EDC_HD ge_p3 ge_mul_by_cofactor(const ge_p3& P) {
   return ge_dbl(ge_dbl(ge_dbl(P, false), false), true);
 }
 
-// dalek IsIdentity on EdwardsPoint: X == 0 and Y == Z (projective)
+// dalek IsIdentity on EdwardsPoint: X == 0 and Y == Z (projective). Z != 0 is also required:
+// every point the complete formulas produce from curve points has Z != 0, so the degenerate
+// (0 : 0 : 0 : 0) can only come from a fault and must never read as the identity.
 EDC_HD bool ge_is_identity(const ge_p3& P) {
-  return fe_is_zero(P.X) && fe_eq(P.Y, P.Z);
+  return fe_is_zero(P.X) && fe_eq(P.Y, P.Z) && !fe_is_zero(P.Z);
 }
 
 EDC_HD void ge_compress(const ge_p3& P, uint32_t w[8]) {
