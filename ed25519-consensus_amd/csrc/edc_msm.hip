@@ -403,20 +403,39 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
                                                                    uint32_t* __restrict__ sorted,
                                                                    const uint32_t* __restrict__ pts,
                                                                    uint32_t* __restrict__ buckets,
-                                                                   uint32_t* __restrict__ heads) {
+                                                                   uint32_t* __restrict__ heads,
+                                                                   uint32_t* __restrict__ slice_W,
+                                                                   uint32_t* __restrict__ slice_T) {
   __shared__ uint32_t lcnt[NSLICE];
   __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
   __shared__ uint32_t lcur[NSLICE];
-  __shared__ __attribute__((aligned(16))) uint32_t lrows[4][WAVE_ROWS_WORDS];
+  // row buffers of the 4 waves during accumulation, then the 256 bucket sums for the reduction
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[NSLICE * EXT_WORDS];
+  static_assert(4 * WAVE_ROWS_WORDS <= NSLICE * EXT_WORDS, "row buffers fit the bucket image");
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
-  if (E == 0) return;
+  if (E == 0) {
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
+    }
+    return;
+  }
   const uint32_t off = offsets[bin];
   lcnt[t] = 0;
   __syncthreads();
-  for (uint32_t e = t; e < E; e += 256) atomicAdd(&lcnt[entries[off + e].y], 1u);
+  // counting sort by bucket; loads are batched 8 deep so the passes are not latency-bound
+  constexpr int SB = 8;
+  for (uint32_t e0 = t; e0 < E; e0 += 256 * SB) {
+    uint32_t y[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) y[u] = e0 + 256u * u < E ? entries[off + e0 + 256u * u].y : 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < SB; ++u)
+      if (y[u] != 0xFFFFFFFFu) atomicAdd(&lcnt[y[u]], 1u);
+  }
   __syncthreads();
   if (t < 64) {
     uint32_t c[4], sum = 0;
@@ -434,9 +453,13 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
   }
   __syncthreads();
   if (lcnt[t] == 0) st_ext(bucket_slot(buckets, bin, t), ge_identity());
-  for (uint32_t e = t; e < E; e += 256) {
-    const uint2 en = entries[off + e];
-    sorted[off + atomicAdd(&lcur[en.y], 1u)] = en.x;
+  for (uint32_t e0 = t; e0 < E; e0 += 256 * SB) {
+    uint2 en[SB];
+#pragma unroll
+    for (int u = 0; u < SB; ++u) en[u] = e0 + 256u * u < E ? entries[off + e0 + 256u * u] : make_uint2(0u, 0xFFFFFFFFu);
+#pragma unroll
+    for (int u = 0; u < SB; ++u)
+      if (en[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[en[u].y], 1u)] = en[u].x;
   }
   __syncthreads();   // workgroup-scope release/acquire: the sorted lists are read back below
   const uint32_t lo = (uint32_t)(((uint64_t)E * t) >> 8), hi = (uint32_t)(((uint64_t)E * (t + 1)) >> 8);
@@ -450,10 +473,43 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
   bool in_head = head0;
   uint32_t cend = lend[cb];
   const uint32_t rounds = __builtin_amdgcn_readfirstlane(((uint64_t)E + 255) >> 8);
-  uint32_t* wrows = lrows[wv];
+  uint32_t* wrows = lbuf + wv * WAVE_ROWS_WORDS;
   uint32_t* my_head = heads + ((size_t)bin * NSLICE + t) * EXT_WORDS;
   ge_p3 acc = ge_identity();
-  uint32_t e_next = lo < hi ? sorted[off + lo] : 0u;
+  // DMA piece map of this lane: instruction k moves piece g - 7 src of the wave's row
+  // src = g / 7, g = 64 k + lane; the seven 6-bit src fields are packed in two registers
+  uint32_t pmap0 = 0, pmap1 = 0;
+#pragma unroll
+  for (int k = 0; k < ROW_PIECES; ++k) {
+    const uint32_t src = (64u * k + lane) / 7u;
+    if (k < 5) pmap0 |= src << (6 * k); else pmap1 |= src << (6 * (k - 5));
+  }
+  // one round of row gathers: the wave's 64 rows (one per lane, `row`) -> wrows, row-major
+  auto gather_rows = [&](uint32_t row) {
+#if EDC_ACC_PROBE == 5      // measurement probe: 64-byte rows (4 pieces, 4 DMA instructions)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t g = 64u * k + lane;
+      const uint32_t r = (uint32_t)__shfl((int)row, (int)(g >> 2), 64);
+      dma_piece(pts + (size_t)r * NIELS_WORDS + (g & 3) * 4, wrows + k * 256);
+    }
+    return;
+#endif
+    asm volatile("" : "+v"(pmap0), "+v"(pmap1));   // unpacked each round, never hoisted (VGPRs)
+#pragma unroll
+    for (int k = 0; k < ROW_PIECES; ++k) {
+      const uint32_t src = k < 5 ? (pmap0 >> (6 * k)) & 63u : (pmap1 >> (6 * (k - 5))) & 63u;
+      const uint32_t piece = 64u * k + lane - 7u * src;
+      const uint32_t r = (uint32_t)__shfl((int)row, (int)src, 64);
+      dma_piece(pts + (size_t)r * NIELS_WORDS + piece * 4, wrows + k * 256);
+    }
+  };
+  // software pipeline: the rows of round j + 1 are in flight while round j's addition runs
+  uint32_t e = lo < hi ? sorted[off + lo] : 0u;
+  uint32_t e_next = lo + 1 < hi ? sorted[off + lo + 1] : e;
+#if EDC_ACC_PROBE != 2 && EDC_ACC_PROBE != 6
+  gather_rows(e & 0x7FFFFFFFu);
+#endif
   for (uint32_t j = 0; j < rounds; ++j) {
     const uint32_t pos = lo + j;
     if (pos < hi && pos == cend) {                 // the running bucket ended: flush it
@@ -463,30 +519,23 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
       do { ++cb; } while (lend[cb] <= pos);        // skip empty buckets
       cend = lend[cb];
     }
-    const uint32_t e = e_next;
-    if (pos + 1 < hi) e_next = sorted[off + pos + 1];
-    const uint32_t row = e & 0x7FFFFFFFu;          // lanes past their range re-read a valid row
-#if EDC_ACC_PROBE == 2      // measurement probe: arithmetic only, no gather (result wrong)
-    ge_niels q = ld_niels(pts, 1 + (row & 1));
+#if EDC_ACC_PROBE == 2 || EDC_ACC_PROBE == 6   // measurement probes: no gather (result wrong)
+    ge_niels q = ld_niels(pts, 1 + (e & 1));
 #else
-    uint32_t lane_o = (uint32_t)lane;
-    asm volatile("" : "+v"(lane_o));               // recompute the piece map each round: hoisted
-#pragma unroll                                     // out of the loop it costs 14 live VGPRs
-    for (int k = 0; k < ROW_PIECES; ++k) {
-      const uint32_t g = 64u * k + lane_o;
-      const uint32_t src = g / 7u, piece = g - 7u * src;
-      const uint32_t r = (uint32_t)__shfl((int)row, (int)src, 64);
-      dma_piece(pts + (size_t)r * NIELS_WORDS + piece * 4, wrows + k * 256);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): this round's rows are in LDS
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): round j's rows are in LDS
     ge_niels q = ld_row_lds(wrows + lane * ROW_WORDS);
+    __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): row in VGPRs before the refill
+    if (j + 1 < rounds) gather_rows(e_next & 0x7FFFFFFFu);   // lanes past their range re-read a row
 #endif
+    const uint32_t e_cur = e;
+    e = e_next;
+    if (pos + 2 < hi) e_next = sorted[off + pos + 2];
     if (pos < hi) {
-#if EDC_ACC_PROBE == 1      // measurement probe: gathers only (result wrong)
+#if EDC_ACC_PROBE == 1 || EDC_ACC_PROBE == 5 || EDC_ACC_PROBE == 6   // probes: no addition (result wrong)
 #pragma unroll
       for (int k = 0; k < 9; ++k) acc.X.v[k] ^= q.ypx.v[k] ^ q.ymx.v[k] ^ q.xy2d.v[k];
 #else
-      if (e >> 31) q = ge_niels_neg(q);
+      if (e_cur >> 31) q = ge_niels_neg(q);
       acc = ge_madd(acc, q);
 #endif
     }
@@ -505,6 +554,20 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
       if (cend <= hi_u) break;                     // with an empty range (E < 256) hold no head
     }
     st_ext(bucket_slot(buckets, bin, cb), acc);
+  }
+  // the bin's reduction (fused: its latency-bound steps overlap the other workgroups of the CU)
+  // W = sum_t (t+1) S_t and T = sum_t S_t over the 256 bucket sums (quad-cooperative)
+  __syncthreads();   // every bucket of the bin is stored
+  st_ext(lbuf + t * EXT_WORDS, ld_ext(bucket_slot(buckets, bin, t)));
+  __syncthreads();
+  ge_p3 ws, tot;
+  weighted_sum_256(lbuf, lbuf, lbuf + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
+  if (t < 4) {
+    ge_p3 W = quad_add(ws, tot);       // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+    }
   }
 }
 
@@ -671,7 +734,8 @@ void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* o
                        uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
 #if EDC_ACC_DMA
   hipLaunchKernelGGL(k_msm_accum_dma, dim3(NBIN), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
-                     heads);
+                     heads, slice_W, slice_T);
+  return;                              // the reduction is fused into the accumulation
 #else
   (void)sorted;
   (void)heads;
