@@ -36,13 +36,12 @@ static const uint64_t SHA512_K[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
-// 64-bit words viewed as 32-bit halves through bit casts (free register-pair views): rotates are
-// two v_alignbit_b32, three-way xors one v_bitop3_b32 per half, adds v_lshl_add_u64.
-struct w64 { uint32_t lo, hi; };
-
-EDC_HD w64 mk64(uint64_t x) { return w64{(uint32_t)x, (uint32_t)(x >> 32)}; }
-EDC_HD uint64_t un64(w64 x) { return ((uint64_t)x.hi << 32) | x.lo; }
-
+// Native 64-bit words: LLVM lowers a 64-bit rotate to two v_alignbit_b32, a three-way xor / ch /
+// maj to one v_bitop3_b32 per half and an add to one v_lshl_add_u64 (64-bit values kept in
+// register pairs; a 32-bit-halves formulation costs v_mov shuffles to rebuild the pairs).
+EDC_HD uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+EDC_HD uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+EDC_HD uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 // funnel shift right of hi:lo by n (0 < n < 32)
 EDC_HD uint32_t fshr32(uint32_t hi, uint32_t lo, int n) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -58,70 +57,65 @@ EDC_HD uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
   return a ^ b ^ c;
 #endif
 }
-EDC_HD w64 rotr(w64 x, int n) {
-  if (n < 32) return w64{fshr32(x.hi, x.lo, n), fshr32(x.lo, x.hi, n)};
-  return w64{fshr32(x.lo, x.hi, n - 32), fshr32(x.hi, x.lo, n - 32)};
+// halves of rotr(x, n) for a compile-time n (one v_alignbit_b32 each)
+template <int N> EDC_HD uint32_t rotr_lo(uint32_t l, uint32_t h) { return N < 32 ? fshr32(h, l, N) : fshr32(l, h, N - 32); }
+template <int N> EDC_HD uint32_t rotr_hi(uint32_t l, uint32_t h) { return N < 32 ? fshr32(l, h, N) : fshr32(h, l, N - 32); }
+// rotr(x, n1) ^ rotr(x, n2) ^ rotr(x, n3): six v_alignbit_b32 + two v_bitop3_b32
+template <int N1, int N2, int N3>
+EDC_HD uint64_t rot3(uint64_t x) {
+  const uint32_t l = lo32(x), h = hi32(x);
+  return mk64(xor3_32(rotr_lo<N1>(l, h), rotr_lo<N2>(l, h), rotr_lo<N3>(l, h)),
+              xor3_32(rotr_hi<N1>(l, h), rotr_hi<N2>(l, h), rotr_hi<N3>(l, h)));
 }
-EDC_HD w64 shr(w64 x, int n) { return w64{fshr32(x.hi, x.lo, n), x.hi >> n}; }
-EDC_HD w64 xor3(w64 a, w64 b, w64 c) { return w64{xor3_32(a.lo, b.lo, c.lo), xor3_32(a.hi, b.hi, c.hi)}; }
-EDC_HD w64 add(w64 a, w64 b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  unsigned int carry;
-  uint32_t lo = __builtin_addc(a.lo, b.lo, 0u, &carry);
-  unsigned int c2;
-  uint32_t hi = __builtin_addc(a.hi, b.hi, carry, &c2);
-  return w64{lo, hi};
-#else
-  return mk64(un64(a) + un64(b));
-#endif
-}
-EDC_HD w64 ch(w64 e, w64 f, w64 g) { return w64{(e.lo & f.lo) ^ (~e.lo & g.lo), (e.hi & f.hi) ^ (~e.hi & g.hi)}; }
-EDC_HD w64 maj(w64 a, w64 b, w64 c) {
-  return w64{(a.lo & b.lo) ^ (a.lo & c.lo) ^ (b.lo & c.lo), (a.hi & b.hi) ^ (a.hi & c.hi) ^ (b.hi & c.hi)};
+// rotr(x, n1) ^ rotr(x, n2) ^ (x >> n3), n3 < 32
+template <int N1, int N2, int N3>
+EDC_HD uint64_t sig_small(uint64_t x) {
+  const uint32_t l = lo32(x), h = hi32(x);
+  return mk64(xor3_32(rotr_lo<N1>(l, h), rotr_lo<N2>(l, h), fshr32(h, l, N3)),
+              xor3_32(rotr_hi<N1>(l, h), rotr_hi<N2>(l, h), h >> N3));
 }
 
 #define EDC_SHA_ROUND(a, b, c, d, e, f, g, h, k, wt)                                              \
   {                                                                                              \
-    w64 t1 = add(add(add(h, xor3(rotr(e, 14), rotr(e, 18), rotr(e, 41))), add(ch(e, f, g), k)), wt); \
-    w64 t2 = add(xor3(rotr(a, 28), rotr(a, 34), rotr(a, 39)), maj(a, b, c));                         \
-    d = add(d, t1);                                                                              \
-    h = add(t1, t2);                                                                             \
+    const uint64_t t1 = h + rot3<14, 18, 41>(e) + ((e & f) ^ (~e & g)) + (k) + (wt);             \
+    const uint64_t t2 = rot3<28, 34, 39>(a) + ((a & b) ^ (a & c) ^ (b & c));                     \
+    d += t1;                                                                                     \
+    h = t1 + t2;                                                                                 \
   }
 
 // 80 rounds as 5 x 16: the 16-round body is unrolled (message words in registers, the eight
 // working variables renamed instead of moved), the 5 passes are a loop.
 EDC_HD void sha512_compress(uint64_t hs[8], const uint64_t win[16]) {
-  w64 w[16];
+  uint64_t w[16];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) w[t] = mk64(win[t]);
-  w64 a = mk64(hs[0]), b = mk64(hs[1]), c = mk64(hs[2]), d = mk64(hs[3]);
-  w64 e = mk64(hs[4]), f = mk64(hs[5]), g = mk64(hs[6]), h = mk64(hs[7]);
+  for (int t = 0; t < 16; ++t) w[t] = win[t];
+  uint64_t a = hs[0], b = hs[1], c = hs[2], d = hs[3], e = hs[4], f = hs[5], g = hs[6], h = hs[7];
 #pragma unroll 1
   for (int r = 0; r < 5; ++r) {
     if (r) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        w64 w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        w64 s0 = xor3(rotr(w15, 1), rotr(w15, 8), shr(w15, 7));
-        w64 s1 = xor3(rotr(w2, 19), rotr(w2, 61), shr(w2, 6));
-        w[j] = add(add(w[j], s0), add(w[(j + 9) & 15], s1));
+        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        const uint64_t s0 = sig_small<1, 8, 7>(w15);
+        const uint64_t s1 = sig_small<19, 61, 6>(w2);
+        w[j] = w[j] + s0 + w[(j + 9) & 15] + s1;
       }
     }
     const uint64_t* K = SHA512_K + 16 * r;
 #pragma unroll
     for (int j = 0; j < 16; j += 8) {
-      EDC_SHA_ROUND(a, b, c, d, e, f, g, h, mk64(K[j + 0]), w[j + 0]);
-      EDC_SHA_ROUND(h, a, b, c, d, e, f, g, mk64(K[j + 1]), w[j + 1]);
-      EDC_SHA_ROUND(g, h, a, b, c, d, e, f, mk64(K[j + 2]), w[j + 2]);
-      EDC_SHA_ROUND(f, g, h, a, b, c, d, e, mk64(K[j + 3]), w[j + 3]);
-      EDC_SHA_ROUND(e, f, g, h, a, b, c, d, mk64(K[j + 4]), w[j + 4]);
-      EDC_SHA_ROUND(d, e, f, g, h, a, b, c, mk64(K[j + 5]), w[j + 5]);
-      EDC_SHA_ROUND(c, d, e, f, g, h, a, b, mk64(K[j + 6]), w[j + 6]);
-      EDC_SHA_ROUND(b, c, d, e, f, g, h, a, mk64(K[j + 7]), w[j + 7]);
+      EDC_SHA_ROUND(a, b, c, d, e, f, g, h, K[j + 0], w[j + 0]);
+      EDC_SHA_ROUND(h, a, b, c, d, e, f, g, K[j + 1], w[j + 1]);
+      EDC_SHA_ROUND(g, h, a, b, c, d, e, f, K[j + 2], w[j + 2]);
+      EDC_SHA_ROUND(f, g, h, a, b, c, d, e, K[j + 3], w[j + 3]);
+      EDC_SHA_ROUND(e, f, g, h, a, b, c, d, K[j + 4], w[j + 4]);
+      EDC_SHA_ROUND(d, e, f, g, h, a, b, c, K[j + 5], w[j + 5]);
+      EDC_SHA_ROUND(c, d, e, f, g, h, a, b, K[j + 6], w[j + 6]);
+      EDC_SHA_ROUND(b, c, d, e, f, g, h, a, K[j + 7], w[j + 7]);
     }
   }
-  hs[0] += un64(a); hs[1] += un64(b); hs[2] += un64(c); hs[3] += un64(d);
-  hs[4] += un64(e); hs[5] += un64(f); hs[6] += un64(g); hs[7] += un64(h);
+  hs[0] += a; hs[1] += b; hs[2] += c; hs[3] += d;
+  hs[4] += e; hs[5] += f; hs[6] += g; hs[7] += h;
 }
 #undef EDC_SHA_ROUND
 
@@ -161,14 +155,16 @@ EDC_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t j) {
   if (j + 8 <= mlen) {
     const uintptr_t p = (uintptr_t)(m + j);
     const uintptr_t a = p & ~(uintptr_t)3;
-    const uint32_t sh = (uint32_t)(p & 3) * 8;
     const uint32_t d0 = ld_dword_at(a), d1 = ld_dword_at(a + 4);
-    uint32_t lo = d0, hi = d1;
-    if (sh) {
-      const uint32_t d2 = ld_dword_at(a + 8);
-      lo = (d0 >> sh) | (d1 << (32 - sh));
-      hi = (d1 >> sh) | (d2 << (32 - sh));
-    }
+    const uint32_t d2 = ld_dword_at((p + 7) & ~(uintptr_t)3);   // = d1 when p is dword aligned
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t sh = (uint32_t)(p & 3);                       // funnel shifts by bytes, no branch
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+#else
+    const uint32_t sh = (uint32_t)(p & 3) * 8;
+    const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
+    const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
+#endif
     return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
   }
   uint64_t w = 0;
