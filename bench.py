@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
-    ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (submit/wait pipelining)")
+    ap.add_argument("--inflight", type=int, default=4, help="batches in flight per GPU (submit/wait pipelining)")
     ap.add_argument("--probe", action="store_true", help="measurement-probe builds: do not require Ok verdicts")
     args = ap.parse_args()
 

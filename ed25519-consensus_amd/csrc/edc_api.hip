@@ -23,7 +23,7 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, count * sizeof(T));
 }
 
-constexpr int kSlots = 2;  // batches that can be in flight per context
+constexpr int kSlots = 4;  // batches that can be in flight per context
 
 }  // namespace
 

@@ -77,7 +77,7 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
 /*
  * Asynchronous form of edc_batch_verify_device for streams of batches (a consensus node
  * verifying block after block): edc_batch_submit_device enqueues the whole pipeline on one of the
- * context's in-flight slots (2) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
+ * context's in-flight slots (4) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
  * ticket and returns its verdict (EDC_OK / EDC_INVALID_SIGNATURE, <0 on runtime failure), with
  * optional check8 (needs want_check8), partial point and bad flag. Tickets must be waited in
  * submission order before their slot is reused; inputs must stay valid until the wait.
