@@ -38,7 +38,8 @@ EDC_MALFORMED_PUBLIC_KEY = 2
 ABI_SYMBOLS = [
     "edc_device_count", "edc_create", "edc_destroy", "edc_last_error", "edc_batch_verify",
     "edc_batch_verify_z", "edc_batch_verify_device", "edc_batch_partial_device", "edc_combine_partials",
-    "edc_batch_submit_device", "edc_batch_wait", "edc_verify_each", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
+    "edc_batch_submit_device", "edc_batch_wait", "edc_verify_each", "edc_verify_each_device",
+    "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize",
 ]
@@ -104,6 +105,8 @@ def load_library(path=None):
                                                 ctypes.c_int]
         lib.edc_batch_wait.argtypes = [c_vp, ctypes.c_int64, c_vp, c_vp, ctypes.POINTER(ctypes.c_int)]
         lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
+        lib.edc_verify_each_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]
+        lib.edc_find_invalid_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_sz, c_vp]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]

@@ -484,6 +484,118 @@ int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* si
   return 0;
 }
 
+int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig, const uint8_t* d_msg,
+                           const uint64_t* d_msg_off, uint8_t* d_verdicts) {
+  if (!ctx || (n && (!d_vk || !d_sig || !d_msg_off || !d_verdicts))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  int rc = ensure_n(ctx, n);
+  if (rc) return rc;
+  if (!n) return 0;
+  hipStream_t st = ctx->st();
+  launch_challenge(st, (uint32_t)n, d_vk, d_sig, d_msg, d_msg_off, ctx->kbuf);
+  launch_verify_single(st, (uint32_t)n, d_vk, d_sig, ctx->kbuf, ctx->btab, d_verdicts);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// ---- grouped fallback (bisection on partial check points) ----
+// sum of g canonical partial points (128-byte records) -> canonical sum, and the verdict of
+// [8]*sum == 0 (with the OR of the bad flags)
+static int sum_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad, uint8_t sum[128]) {
+  int rc = ensure_aux(ctx, g * 128 + 1);
+  if (rc) return rc;
+  Slot& s = ctx->slot[0];
+  CK(hipMemcpyAsync(ctx->aux, partials, g * 128, hipMemcpyHostToDevice, s.st));
+  CK(hipMemsetAsync(s.d_out, 0, 256, s.st));
+  launch_combine(s.st, (uint32_t)g, ctx->aux, bad, 0, s.d_out);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, s.st));
+  s.pending = true;
+  s.timed = false;
+  return finish_batch(ctx, s, nullptr, sum, nullptr);
+}
+
+// canonical -P from canonical P (x -> p - x on X and T)
+static void neg_partial(const uint8_t P[128], uint8_t out[128]) {
+  static const uint8_t pbytes[32] = {0xed, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                     0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                     0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f};
+  memcpy(out, P, 128);
+  for (int c : {0, 3}) {
+    const uint8_t* x = P + 32 * c;
+    bool zero = true;
+    for (int i = 0; i < 32; ++i) zero &= x[i] == 0;
+    if (zero) continue;
+    int borrow = 0;
+    for (int i = 0; i < 32; ++i) {
+      int d = (int)pbytes[i] - x[i] - borrow;
+      borrow = d < 0;
+      out[32 * c + i] = (uint8_t)(d + (borrow ? 256 : 0));
+    }
+  }
+}
+
+int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                            const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                            size_t leaf, uint8_t* verdicts) {
+  if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_msg_off || !verdicts))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  if (ctx->slot[0].pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
+  if (leaf < 64) leaf = 64;
+  memset(verdicts, 0, n);
+  if (!n) return 0;
+  struct Node { size_t lo, hi; int bad; uint8_t P[128]; };
+  auto partial = [&](size_t lo, size_t hi, Node& nd) -> int {
+    nd.lo = lo; nd.hi = hi;
+    return run_batch_sync(ctx, hi - lo, d_vk + 32 * lo, d_sig + 64 * lo, d_msg, d_msg_off + lo, z_seed, lo, nullptr,
+                          nullptr, nd.P, &nd.bad);
+  };
+  std::vector<Node> todo(1);
+  int rc = partial(0, n, todo[0]);
+  if (rc < 0) return rc;
+  if (rc == 0) { todo.clear(); }
+  int invalid = 0;
+  while (!todo.empty()) {
+    Node nd = todo.back();
+    todo.pop_back();
+    const size_t m = nd.hi - nd.lo;
+    if (m <= leaf) {   // per-item Item::verify_single on the leaf
+      rc = ensure_n(ctx, m);
+      if (rc) return rc;
+      hipStream_t st = ctx->st();
+      launch_challenge(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, d_msg, d_msg_off + nd.lo, ctx->kbuf);
+      launch_verify_single(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, ctx->kbuf, ctx->btab,
+                           ctx->verdicts);
+      CK(hipGetLastError());
+      CK(hipMemcpyAsync(verdicts + nd.lo, ctx->verdicts, m, hipMemcpyDeviceToHost, st));
+      CK(hipStreamSynchronize(st));
+      for (size_t i = 0; i < m; ++i) invalid += verdicts[nd.lo + i] != 0;
+      continue;
+    }
+    const size_t mid = nd.lo + m / 2;
+    Node L, R;
+    rc = partial(nd.lo, mid, L);
+    if (rc < 0) return rc;
+    const int bad_l = rc;
+    int bad_r;
+    if (nd.bad) {      // a decode / canonicity failure makes the parent's point meaningless
+      bad_r = partial(mid, nd.hi, R);
+      if (bad_r < 0) return bad_r;
+    } else {           // linearity: P_R = P - P_L, no item of either half failed decoding
+      uint8_t pair[256];
+      memcpy(pair, nd.P, 128);
+      neg_partial(L.P, pair + 128);
+      R.lo = mid; R.hi = nd.hi; R.bad = 0;
+      bad_r = sum_partials(ctx, 2, pair, 0, R.P);
+      if (bad_r < 0) return bad_r;
+    }
+    if (bad_r) todo.push_back(R);
+    if (bad_l) todo.push_back(L);
+  }
+  return invalid;
+}
+
 int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok) {
   if (!ctx || (n && (!enc || !xy || !ok))) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));

@@ -115,6 +115,22 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
 int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
                     const uint8_t* msg, const uint64_t* msg_off, uint8_t* verdicts);
 
+/* Device-resident edc_verify_each: verdicts into d_verdicts (n bytes of this GPU's memory). */
+int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                           const uint8_t* d_msg, const uint64_t* d_msg_off, uint8_t* d_verdicts);
+
+/*
+ * Grouped fallback after a failed batch (the caller-driven Item::verify_single loop of
+ * reference tests/batch.rs:37-43, src/batch.rs:104-107, done by bisection): the batch equation is
+ * linear, so a range's check point minus its left half's is its right half's; ranges whose
+ * [8]*check is the identity are valid (ZIP215: batch == single), failing ranges are halved
+ * until <= leaf items, which are verified one by one. verdicts (host, n bytes) equal
+ * Item::verify_single's code for every item. Returns the number of invalid items, or <0.
+ */
+int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                            const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                            size_t leaf, uint8_t* verdicts);
+
 /*
  * batch::Item::verify_single (reference src/batch.rs:104-107): as edc_verify_each but with the
  * queue-time challenge k (n*32 bytes, canonical scalars) instead of the message.
