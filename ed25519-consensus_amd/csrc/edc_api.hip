@@ -63,6 +63,7 @@ struct edc_ctx {
   uint64_t* off = nullptr;
   uint32_t* kbuf = nullptr;
   uint8_t* verdicts = nullptr;
+  uint32_t* vtab = nullptr;     // per-item multiples tables of the per-signature kernel
   uint8_t* aux = nullptr;       // decode xy / sign outputs / partials
   bool timing = false;
   float last_ms[PH_N] = {};
@@ -152,10 +153,11 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
 static int ensure_n(edc_ctx* ctx, size_t n) {
   if (n <= ctx->cap_n && ctx->vk) return 0;
   CK(hipStreamSynchronize(ctx->st()));
-  void* ptrs[] = {ctx->vk, ctx->sig, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts};
+  void* ptrs[] = {ctx->vk, ctx->sig, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   const size_t cap = n < 1024 ? 1024 : n + n / 8;
+  CK(dalloc(&ctx->vtab, verify_single_scratch_words(cap)));
   CK(dalloc(&ctx->vk, cap * 32));
   CK(dalloc(&ctx->sig, cap * 64));
   CK(dalloc(&ctx->zexp, cap * 16));
@@ -351,7 +353,8 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.side) (void)hipStreamDestroy(s.side);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
-  void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->aux, ctx->btab};
+  void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
+                  ctx->btab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete ctx;
@@ -461,7 +464,7 @@ int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const u
   CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->kbuf, k, n * 32, hipMemcpyHostToDevice, st));
-  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts);
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
@@ -477,7 +480,7 @@ int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* si
   if (!n) return 0;
   hipStream_t st = ctx->st();
   launch_challenge(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->kbuf);
-  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts);
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
@@ -493,7 +496,7 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
   if (!n) return 0;
   hipStream_t st = ctx->st();
   launch_challenge(st, (uint32_t)n, d_vk, d_sig, d_msg, d_msg_off, ctx->kbuf);
-  launch_verify_single(st, (uint32_t)n, d_vk, d_sig, ctx->kbuf, ctx->btab, d_verdicts);
+  launch_verify_single(st, (uint32_t)n, d_vk, d_sig, ctx->kbuf, ctx->btab, ctx->vtab, d_verdicts);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));
   return 0;
@@ -565,7 +568,7 @@ int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
       if (rc) return rc;
       hipStream_t st = ctx->st();
       launch_challenge(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, d_msg, d_msg_off + nd.lo, ctx->kbuf);
-      launch_verify_single(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, ctx->kbuf, ctx->btab,
+      launch_verify_single(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, ctx->kbuf, ctx->btab, ctx->vtab,
                            ctx->verdicts);
       CK(hipGetLastError());
       CK(hipMemcpyAsync(verdicts + nd.lo, ctx->verdicts, m, hipMemcpyDeviceToHost, st));

@@ -32,7 +32,8 @@ size_t msm_entry_capacity(uint32_t n);
 // edc_single.hip
 void launch_init_btable(hipStream_t st, uint32_t* btab);
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
-                          const uint32_t* k, const uint32_t* btab, uint8_t* verdict);
+                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict);
+size_t verify_single_scratch_words(size_t n);
 void launch_sign(hipStream_t st, uint32_t n, const uint8_t* seeds, const uint32_t* seed_index,
                  const uint8_t* msg, const uint64_t* off, const uint32_t* btab, uint8_t* vk_out,
                  uint8_t* sig_out);

@@ -42,6 +42,31 @@ __device__ __forceinline__ void radix16(const uint32_t s[8], int8_t d[64]) {
   }
 }
 
+// the same recoding without a digit array: bit j of the mask is the carry out of position j
+// (digit j was lowered by 16); digit j = nibble j + carry in - 16 carry out
+__device__ __forceinline__ uint64_t radix16_carries(const uint32_t s[8]) {
+  uint64_t m = 0;
+  uint32_t carry = 0;
+  for (int j = 0; j < 63; ++j) {
+    const uint32_t v = ((s[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
+    carry = v > 8;
+    m |= (uint64_t)carry << j;
+  }
+  return m;
+}
+// s[w] for a runtime w as a select chain (a runtime-indexed register array goes to scratch)
+__device__ __forceinline__ uint32_t word_at(const uint32_t s[8], int w) {
+  uint32_t r = s[0];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) r = w == q ? s[q] : r;
+  return r;
+}
+__device__ __forceinline__ int radix16_digit(const uint32_t s[8], uint64_t carries, int j) {
+  const int nib = (int)((word_at(s, j >> 3) >> (4 * (j & 7))) & 15u);
+  const int cin = j ? (int)((carries >> (j - 1)) & 1) : 0;
+  return nib + cin - 16 * (int)((carries >> j) & 1);
+}
+
 __device__ __forceinline__ ge_cached cached_identity() {
   ge_cached c; c.ypx = fe_one(); c.ymx = fe_one(); c.Z = fe_one(); c.T2d = fe_zero(); return c;
 }
@@ -53,21 +78,22 @@ __device__ __forceinline__ ge_cached ld_cached(const uint32_t* p) {
   ge_cached c; c.ypx = ld_fe(p); c.ymx = ld_fe(p + 9); c.Z = ld_fe(p + 18); c.T2d = ld_fe(p + 27); return c;
 }
 
-constexpr int SV_THREADS = 64;
+constexpr int SV_THREADS = 256;
+constexpr int SV_TAB_WORDS = 9 * EXT_WORDS;   // per-item [1..8]P (projective Niels) + R parked
 
-// R' = [k]P + [s]B with P's table in LDS (8 cached multiples per lane), B from btab.
+// R' = [k]P + [s]B, signed radix-16 windows. P's table of 8 cached multiples lives in the
+// item's global scratch record (LDS for 8 x 144 bytes per lane held 0.5 waves per SIMD); B's
+// affine Niels multiples come from the context table.
 __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const uint32_t s[8],
-                                   const uint32_t* btab, uint32_t* ltab) {
+                                   const uint32_t* btab, uint32_t* tab) {
   ge_cached c = ge_to_cached(P);
   ge_p3 acc = P;
-  st_cached(ltab, c);
+  st_cached(tab, c);
   for (int i = 1; i < 8; ++i) {
     acc = ge_add_cached(acc, c);
-    st_cached(ltab + i * EXT_WORDS * SV_THREADS, ge_to_cached(acc));
+    st_cached(tab + i * EXT_WORDS, ge_to_cached(acc));
   }
-  int8_t kd[64], sd[64];
-  radix16(k, kd);
-  radix16(s, sd);
+  const uint64_t kc = radix16_carries(k), sc = radix16_carries(s);
   acc = ge_identity();
   for (int j = 63; j >= 0; --j) {
     if (j != 63) {
@@ -76,12 +102,13 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
       acc = ge_dbl(acc, false);
       acc = ge_dbl(acc, true);
     }
-    int a = kd[j];
+    int a = radix16_digit(k, kc, j);
     int ai = a < 0 ? -a : a;
-    ge_cached q = ai ? ld_cached(ltab + (ai - 1) * EXT_WORDS * SV_THREADS) : cached_identity();
+    ge_cached q = ai ? ld_cached(tab + (ai - 1) * EXT_WORDS) : cached_identity();
     if (a < 0) q = ge_cached_neg(q);
     acc = ge_add_cached(acc, q);
-    int b = sd[j];
+    EDC_SCHED_FENCE();
+    int b = radix16_digit(s, sc, j);
     int bi = b < 0 ? -b : b;
     ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
     if (b < 0) nb = ge_niels_neg(nb);
@@ -91,12 +118,12 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
 }
 
 // verdict codes: 0 Ok, 1 InvalidSignature, 2 MalformedPublicKey
-__global__ void __launch_bounds__(SV_THREADS) k_verify_single(uint32_t n, const uint8_t* __restrict__ vk,
-                                                              const uint8_t* __restrict__ sig,
-                                                              const uint32_t* __restrict__ kscal,
-                                                              const uint32_t* __restrict__ btab,
-                                                              uint8_t* __restrict__ verdict) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+__global__ void __launch_bounds__(SV_THREADS, 3) k_verify_single(uint32_t n, const uint8_t* __restrict__ vk,
+                                                                 const uint8_t* __restrict__ sig,
+                                                                 const uint32_t* __restrict__ kscal,
+                                                                 const uint32_t* __restrict__ btab,
+                                                                 uint32_t* __restrict__ vtab,
+                                                                 uint8_t* __restrict__ verdict) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
@@ -108,13 +135,17 @@ __global__ void __launch_bounds__(SV_THREADS) k_verify_single(uint32_t n, const 
   if (!sc_is_canonical(sw)) { verdict[i] = 1; return; }          // s checked before R
   uint32_t rw[8];
   ld_words8(sig + (size_t)i * 64, rw);
-  ge_p3 R;
-  if (!ge_decompress(rw, R)) { verdict[i] = 1; return; }
+  uint32_t* tab = vtab + (size_t)i * SV_TAB_WORDS;
+  {
+    ge_p3 R;
+    if (!ge_decompress(rw, R)) { verdict[i] = 1; return; }
+    st_ext(tab + 8 * EXT_WORDS, R);    // parked in the scratch record: not live across the loop
+  }
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
-  ge_p3 Rp = double_scalar_mul(k, ge_neg(A), sw, btab, smem + threadIdx.x * EXT_WORDS);
-  ge_p3 d = ge_add(R, ge_neg(Rp));
+  ge_p3 Rp = double_scalar_mul(k, ge_neg(A), sw, btab, tab);
+  ge_p3 d = ge_add(ld_ext(tab + 8 * EXT_WORDS), ge_neg(Rp));
   verdict[i] = ge_is_identity(ge_mul_by_cofactor(d)) ? 0 : 1;
 }
 
@@ -229,12 +260,12 @@ void launch_init_btable(hipStream_t st, uint32_t* btab) {
   hipLaunchKernelGGL(k_init_btable, dim3(1), dim3(64), 0, st, btab);
 }
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
-                          const uint32_t* k, const uint32_t* btab, uint8_t* verdict) {
+                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict) {
   if (!n) return;
-  size_t lds = (size_t)8 * EXT_WORDS * SV_THREADS * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), lds, st, n, vk, sig, k,
-                     btab, verdict);
+  hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, btab,
+                     vtab, verdict);
 }
+size_t verify_single_scratch_words(size_t n) { return n * SV_TAB_WORDS; }
 void launch_sign(hipStream_t st, uint32_t n, const uint8_t* seeds, const uint32_t* seed_index,
                  const uint8_t* msg, const uint64_t* off, const uint32_t* btab, uint8_t* vk_out,
                  uint8_t* sig_out) {

@@ -121,13 +121,22 @@ EDC_HD ge_p3 ge_madd(const ge_p3& P, const ge_niels& q) {
 // P + Q, Q projective Niels: 8M
 EDC_HD ge_p3 ge_add_cached(const ge_p3& P, const ge_cached& q) {
   fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  EDC_SCHED_FENCE();
   fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
+  EDC_SCHED_FENCE();
   fe C = fe_mul(P.T, q.T2d);
+  EDC_SCHED_FENCE();
   fe ZZ = fe_mul(P.Z, q.Z);
   fe D = fe_add_c(ZZ, ZZ);
   fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
   ge_p3 r;
-  r.X = fe_mul(E, F); r.Y = fe_mul(G, H); r.T = fe_mul(E, H); r.Z = fe_mul(F, G);
+  r.X = fe_mul(E, F);
+  EDC_SCHED_FENCE();
+  r.Y = fe_mul(G, H);
+  EDC_SCHED_FENCE();
+  r.T = fe_mul(E, H);
+  EDC_SCHED_FENCE();
+  r.Z = fe_mul(F, G);
   return r;
 }
 
@@ -138,8 +147,11 @@ EDC_HD ge_p3 ge_add(const ge_p3& P, const ge_p3& Q) { return ge_add_cached(P, ge
 // skips T3 for chains of doublings whose T is never read.
 EDC_HD ge_p3 ge_dbl(const ge_p3& P, bool with_t = true) {
   fe XX = fe_sqr(P.X);
+  EDC_SCHED_FENCE();
   fe YY = fe_sqr(P.Y);
+  EDC_SCHED_FENCE();
   fe ZZ = fe_sqr(P.Z);
+  EDC_SCHED_FENCE();
   fe ZZ2 = fe_add(ZZ, ZZ);
   fe XpY2 = fe_sqr(fe_add(P.X, P.Y));
   fe Yc = fe_add(YY, XX);
@@ -148,7 +160,9 @@ EDC_HD ge_p3 ge_dbl(const ge_p3& P, bool with_t = true) {
   fe Tc = fe_sub(ZZ2, Zc);
   ge_p3 r;
   r.X = fe_mul(Xc, Tc);
+  EDC_SCHED_FENCE();
   r.Y = fe_mul(Yc, Zc);
+  EDC_SCHED_FENCE();
   r.Z = fe_mul(Zc, Tc);
   r.T = with_t ? fe_mul(Xc, Yc) : fe_zero();
   return r;

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--keys", type=int, default=150)
     ap.add_argument("--msg-len", type=int, default=120)
-    ap.add_argument("--leaf", type=int, default=16384)
+    ap.add_argument("--leaf", type=int, default=65536)
     args = ap.parse_args()
     import torch
     import bench
