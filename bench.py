@@ -252,6 +252,8 @@ def main():
                          "traffic": traffic,
                          "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": units,
                          "avg_launch_ms": dom_ms},
+            "hbm_view": ({"achieved_gbs": round(traffic / (dom_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+                          "frac": round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if traffic else None),
             "phases_ms": phases,
             "cpu_baseline": cpu,
             "gen_s": round(t_gen, 2),
