@@ -251,7 +251,10 @@ def main():
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
                          "traffic": traffic,
                          "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": units,
-                         "avg_launch_ms": dom_ms},
+                         "avg_launch_ms": dom_ms,
+                         "measured": f"HIP events on the slot stream around each launch, {max(1, args.profile_steps)} "
+                                     "instrumented batches run one at a time after the timed region "
+                                     "(rocprof cross-check: profiles/r01_kernel_stats_inflight1.csv)"},
             "hbm_view": ({"achieved_gbs": round(traffic / (dom_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
                           "frac": round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if traffic else None),
             "phases_ms": phases,
