@@ -12,8 +12,8 @@ using namespace edc;
 namespace {
 
 // phases in enqueue order (each bracketed by HIP events on the slot stream)
-enum Phase { PH_CHALLENGE, PH_KEYS, PH_DECOMP, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
-const char* kPhaseNames[PH_N] = {"challenge_sha512", "keys_group", "decompress_R",
+enum Phase { PH_KEYS, PH_CHALLENGE, PH_DECOMP, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
+const char* kPhaseNames[PH_N] = {"keys_group", "challenge_sha512", "decompress_R",
                                  "coef_chacha_scalar", "msm_bin", "msm_bucket", "msm_window_final"};
 
 template <typename T>
@@ -252,17 +252,18 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
   CK(hipMemsetAsync(s.u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
   CK(hipMemsetAsync(s.d_out, 0, 256, st));
-  mark(PH_CHALLENGE);
-  launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_KEYS);
   launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
               s.pts, s.key_acc, s.flags);
   // fork: distinct keys are decoded (and, few-key mode, shifted by 2^128) on the side stream
-  // while the main stream decodes the R_i; joined before the bucket accumulation reads them
+  // while the main stream hashes and decodes the R_i; joined before the bucket accumulation
+  // reads them
   CK(hipEventRecord(s.fork, st));
   CK(hipStreamWaitEvent(s.side, s.fork, 0));
   launch_key_points(s.side, N, d_vk, s.key_rep, s.pts, ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags);
   CK(hipEventRecord(s.join, s.side));
+  mark(PH_CHALLENGE);
+  launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_DECOMP);
   launch_decompress(st, N, d_sig, s.pts, s.flags);
   mark(PH_COEF);
