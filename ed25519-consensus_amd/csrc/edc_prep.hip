@@ -14,7 +14,10 @@
 
 namespace edc {
 
-__global__ void __launch_bounds__(256, 4) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
+#ifndef EDC_SHA_WAVES
+#define EDC_SHA_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, EDC_SHA_WAVES) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
                                                    const uint8_t* __restrict__ sig,
                                                    const uint8_t* __restrict__ msg,
                                                    const uint64_t* __restrict__ off,
