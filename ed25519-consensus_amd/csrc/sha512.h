@@ -75,10 +75,29 @@ EDC_HD uint64_t sig_small(uint64_t x) {
               xor3_32(rotr_hi<N1>(l, h), rotr_hi<N2>(l, h), h >> N3));
 }
 
+// ch and maj as one v_bitop3_b32 per half (truth tables 0xCA and 0xE8 over (S0, S1, S2));
+// LLVM otherwise emits bfi + and / four ands and xors
+EDC_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return mk64(__builtin_amdgcn_bitop3_b32(lo32(e), lo32(f), lo32(g), 0xCA),
+              __builtin_amdgcn_bitop3_b32(hi32(e), hi32(f), hi32(g), 0xCA));
+#else
+  return (e & f) ^ (~e & g);
+#endif
+}
+EDC_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return mk64(__builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), 0xE8),
+              __builtin_amdgcn_bitop3_b32(hi32(a), hi32(b), hi32(c), 0xE8));
+#else
+  return (a & b) ^ (a & c) ^ (b & c);
+#endif
+}
+
 #define EDC_SHA_ROUND(a, b, c, d, e, f, g, h, k, wt)                                              \
   {                                                                                              \
-    const uint64_t t1 = h + rot3<14, 18, 41>(e) + ((e & f) ^ (~e & g)) + (k) + (wt);             \
-    const uint64_t t2 = rot3<28, 34, 39>(a) + ((a & b) ^ (a & c) ^ (b & c));                     \
+    const uint64_t t1 = h + rot3<14, 18, 41>(e) + ch64(e, f, g) + (k) + (wt);                     \
+    const uint64_t t2 = rot3<28, 34, 39>(a) + maj64(a, b, c);                                     \
     d += t1;                                                                                     \
     h = t1 + t2;                                                                                 \
   }
