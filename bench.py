@@ -52,14 +52,32 @@ def chacha_device(pkg, eng, torch, key, blk0, nblocks, dev):
 
 
 def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
-    """Signed synthetic votes for global queue indices [global_base, global_base + n)."""
-    seeds = chacha_device(pkg, eng, torch, bytes([0x11]) * 32, 0, (keys * 32 + 63) // 64, dev)[: keys * 32]
-    stride = (msg_len + 63) // 64 * 64
-    blocks_per_msg = stride // 64
-    raw = chacha_device(pkg, eng, torch, bytes([0x22]) * 32, global_base * blocks_per_msg, n * blocks_per_msg, dev)
-    msg = raw.view(n, stride)[:, :msg_len].contiguous().view(-1) if n else raw[:1]
-    off = torch.arange(0, n + 1, dtype=torch.int64, device=dev) * msg_len
-    idx = ((torch.arange(global_base, global_base + n, dtype=torch.int64, device=dev)) % keys).to(torch.int32)
+    """Signed synthetic items for global queue indices [global_base, global_base + n).
+    keys > 0: item i is signed by validator i mod keys; keys == 0: every item has its own key.
+    msg_len >= 0: fixed-length messages; msg_len < 0: lengths uniform in [0, 1024] (configs[4])."""
+    if keys > 0:
+        seeds = chacha_device(pkg, eng, torch, bytes([0x11]) * 32, 0, (keys * 32 + 63) // 64, dev)[: keys * 32]
+        idx = ((torch.arange(global_base, global_base + n, dtype=torch.int64, device=dev)) % keys).to(torch.int32)
+    else:                                            # distinct keys: seed of global item i
+        assert global_base % 2 == 0
+        seeds = chacha_device(pkg, eng, torch, bytes([0x11]) * 32, global_base // 2, (n + 1) // 2, dev)[: n * 32]
+        idx = torch.arange(0, n, dtype=torch.int32, device=dev)
+    if msg_len >= 0:
+        stride = (msg_len + 63) // 64 * 64
+        blocks_per_msg = stride // 64
+        raw = chacha_device(pkg, eng, torch, bytes([0x22]) * 32, global_base * blocks_per_msg, n * blocks_per_msg, dev)
+        msg = raw.view(n, stride)[:, :msg_len].contiguous().view(-1) if n else raw[:1]
+        off = torch.arange(0, n + 1, dtype=torch.int64, device=dev) * msg_len
+    else:
+        lens = chacha_device(pkg, eng, torch, bytes([0x55]) * 32, global_base // 32, (n + 31) // 32 + 1, dev)
+        lens = lens.view(torch.int16)[: n].to(torch.int64).abs() % 1025
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(lens, 0)
+        raw = chacha_device(pkg, eng, torch, bytes([0x22]) * 32, global_base * 16, n * 16, dev).view(n, 1024)
+        cols = torch.arange(1024, device=dev)[None, :]
+        chunk = 1 << 18                              # boolean masks stay below 2^31 elements
+        msg = torch.cat([raw[c:c + chunk][cols < lens[c:c + chunk, None]] for c in range(0, n, chunk)] +
+                        [torch.zeros(1, dtype=torch.uint8, device=dev)])
     vk = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=dev)
     sig = torch.empty(max(n, 1) * 64, dtype=torch.uint8, device=dev)
     rc = eng.lib.edc_sign_device(eng.ctx, n, ctypes.c_void_p(seeds.data_ptr()), ctypes.c_void_p(idx.data_ptr()),
@@ -69,9 +87,9 @@ def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
     return vk, sig, msg, off
 
 
-def cpu_baseline(vk, sig, msg, n_sample, keys, msg_len):
+def cpu_baseline(vk, sig, msg, off, n_sample, keys, msg_len):
     """Oracle C restatement (dalek u64-backend algorithm, oracle/edc_oracle.c) on the host
-    cores: the first n_sample signatures of the SAME GPU-generated workload, one Verifier per
+    cores: the first n_sample items of the SAME GPU-generated workload, one Verifier per
     thread over equal contiguous chunks, queue (SHA-512 + grouping) + verify timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
@@ -81,10 +99,18 @@ def cpu_baseline(vk, sig, msg, n_sample, keys, msg_len):
     n_sample = min(n_sample, vk.numel() // 32)
     vkb = vk[: 32 * n_sample].cpu().numpy().tobytes()
     sgb = sig[: 64 * n_sample].cpu().numpy().tobytes()
-    mb = msg[: msg_len * n_sample].cpu().numpy().tobytes()
+    o = off[: n_sample + 1].cpu().tolist()
+    mb = msg[: o[-1]].cpu().numpy().tobytes()
     data = ([vkb[32 * i:32 * i + 32] for i in range(n_sample)], [sgb[64 * i:64 * i + 64] for i in range(n_sample)],
-            [mb[msg_len * i:msg_len * (i + 1)] for i in range(n_sample)])
+            [mb[o[i]:o[i + 1]] for i in range(n_sample)])
     return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len, data=data)
+
+
+CONFIGS = {   # BASELINE.json configs: (items per GPU, validators (0 = distinct keys), message bytes (-1 = 0..1024))
+    "c2": (1 << 16, 0, 32, "configs[1]: 2^16 sigs, distinct keys, 32-byte msgs"),
+    "c3": (1 << 20, 150, 120, "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs"),
+    "c5": (1 << 21, 0, -1, "configs[4]: 2^21 sigs/GPU (2^24 over 8 GPUs), distinct keys, 0..1024-byte msgs"),
+}
 
 
 def main():
@@ -92,15 +118,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="signatures per GPU per step")
-    ap.add_argument("--keys", type=int, default=150)
-    ap.add_argument("--msg-len", type=int, default=120)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="workload; c3 (configs[2]) is the one BASELINE.json's metric is quoted on")
+    ap.add_argument("--n", type=int, default=None, help="signatures per GPU per step (default: the config's)")
+    ap.add_argument("--keys", type=int, default=None, help="validators (0 = distinct keys; default: the config's)")
+    ap.add_argument("--msg-len", type=int, default=None, help="message bytes (-1 = uniform 0..1024)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight per GPU (submit/wait pipelining)")
     ap.add_argument("--probe", action="store_true", help="measurement-probe builds: do not require Ok verdicts")
     args = ap.parse_args()
+    c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
+    args.n = c_n if args.n is None else args.n
+    args.keys = c_keys if args.keys is None else args.keys
+    args.msg_len = c_len if args.msg_len is None else args.msg_len
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,7 +260,7 @@ def main():
                 traffic = None
         cpu = None
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(vk, sig, msg, args.cpu_sample, args.keys, args.msg_len)
+            cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
         line = {
             "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
             "value": round(value, 1),
@@ -242,8 +274,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u32/u64 integer (GF(2^255-19), radix 2^29 limbs)",
             "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
-            "config": {"workload": "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs",
-                       "sigs_per_gpu": n, "validators": args.keys, "msg_len": args.msg_len,
+            "config": {"workload": c_desc,
+                       "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
                        "inflight": args.inflight if world == 1 else 1,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",

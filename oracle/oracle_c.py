@@ -99,5 +99,7 @@ def baseline_c3(n_sample=8192, keys=150, msg_len=120, data=None):
     secs, ok, threads = baseline(vks, sigs, msgs, threads=threads)
     return {"value": round(len(vks) / secs, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
             "ok": ok, "seconds": round(secs, 3),
-            "sample": f"{len(vks)} sigs of the same workload ({keys} validators, {msg_len}-byte msgs), "
+            "sample": f"{len(vks)} sigs of the same workload ("
+                      f"{f'{keys} validators' if keys else 'distinct keys'}, "
+                      f"{f'{msg_len}-byte' if msg_len >= 0 else '0..1024-byte'} msgs), "
                       f"one Verifier per thread over {threads} equal chunks, queue+verify timed"}
