@@ -139,10 +139,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # EDC_DIST_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing the
+    # visible GPUs (the all-gather then goes through host memory); the default is RCCL
+    backend = os.environ.get("EDC_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        dist.init_process_group(backend=backend)
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     torch.zeros(1, device=dev)                     # initialise torch's HIP runtime first
@@ -163,49 +168,39 @@ def main():
     check8 = ctypes.create_string_buffer(32)
 
     pending = []
+    combine = (lambda p, b: eng.combine_partials(p, b, want_check8=False))
+    allgather = sharded.torch_allgather_fn(dist, dev if backend != "gloo" else torch.device("cpu")) if dist else None
 
     def submit():
         t = lib.edc_batch_submit_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
-                                        zseed, 0, None, 0)
+                                        zseed, base, None, 0)
         if t < 0:
             eng._check(t)
         pending.append(t)
 
     def wait_oldest():
-        rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
-        return eng._check(rc)
+        if world == 1:
+            rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
+            return eng._check(rc)
+        # multi-GPU: this rank's partial point of the global batch, all-gathered (RCCL) and combined
+        part = ctypes.create_string_buffer(128)
+        bad = ctypes.c_int(0)
+        eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, part, ctypes.byref(bad)))
+        code, _ = sharded.verify_sharded(lambda zb: (part.raw, bad.value), combine, allgather, rank, world, base)
+        return code
 
     def run_steps(k):
-        """k full batch verifications; with --inflight 2 batch i+1 is enqueued before batch i's
-        verdict is collected (the verdict of every batch is still waited for inside the loop)."""
-        if world > 1 or args.inflight <= 1:
-            return [step() for _ in range(k)]
+        """k full batch verifications; with --inflight F, batch i+F-1 is enqueued before batch i's
+        verdict is collected (every verdict is still waited for inside the loop). Multi-GPU: each
+        collected batch's partial point is all-gathered and combined while the later batches run."""
         codes = []
         for _ in range(k):
-            if len(pending) >= args.inflight:
+            if len(pending) >= max(1, args.inflight):
                 codes.append(wait_oldest())
             submit()
         while pending:
             codes.append(wait_oldest())
         return codes
-
-    def step():
-        if world == 1:
-            # Verifier::verify returns only Ok/Err: no [8]*check compression in the timed loop
-            rc = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
-                                             off.data_ptr(), zseed, 0, None, None)
-            return eng._check(rc)
-
-        def partial(zbase):
-            part = ctypes.create_string_buffer(128)
-            bad = ctypes.c_int(0)
-            eng._check(lib.edc_batch_partial_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
-                                                    off.data_ptr(), zseed, zbase, None, part, ctypes.byref(bad)))
-            return part.raw, bad.value
-
-        code, _ = sharded.verify_sharded(partial, lambda p, b: eng.combine_partials(p, b, want_check8=False),
-                                         sharded.torch_allgather_fn(dist, dev), rank, world, base)
-        return code
 
     eng._check(lib.edc_reserve(eng.ctx, n))        # both in-flight slots' workspaces, before any step
     run_steps(args.warmup)
@@ -220,7 +215,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if not args.probe:
@@ -276,7 +271,7 @@ def main():
             "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
             "config": {"workload": c_desc,
                        "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
-                       "inflight": args.inflight if world == 1 else 1,
+                       "inflight": args.inflight,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

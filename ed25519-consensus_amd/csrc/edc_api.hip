@@ -65,6 +65,10 @@ struct edc_ctx {
   uint8_t* verdicts = nullptr;
   uint32_t* vtab = nullptr;     // per-item multiples tables of the per-signature kernel
   uint8_t* aux = nullptr;       // decode xy / sign outputs / partials
+  // shard-partial combination on its own stream, so it never waits behind in-flight batches
+  Slot comb;
+  uint8_t* comb_in = nullptr;   // g x 128-byte partial records
+  size_t comb_cap = 0;
   bool timing = false;
   float last_ms[PH_N] = {};
   int nlast = 0;
@@ -354,8 +358,21 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.side) (void)hipStreamDestroy(s.side);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
+  {
+    Slot& s = ctx->comb;
+    if (s.st) (void)hipStreamSynchronize(s.st);
+    if (s.flags) (void)hipFree(s.flags);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    for (int p = 0; p <= PH_N; ++p)
+      if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
+    if (s.fork) (void)hipEventDestroy(s.fork);
+    if (s.join) (void)hipEventDestroy(s.join);
+    if (s.side) (void)hipStreamDestroy(s.side);
+    if (s.st) (void)hipStreamDestroy(s.st);
+  }
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
-                  ctx->btab};
+                  ctx->btab, ctx->comb_in};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete ctx;
@@ -423,21 +440,33 @@ int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const 
   return rc < 0 ? rc : 0;
 }
 
-int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad_any, uint8_t check8[32]) {
-  if (!ctx || (g && !partials)) return EDC_ERR_ARG;
-  CK(hipSetDevice(ctx->device));
-  int rc = ensure_aux(ctx, g * 128 + 1);
+// sum of g canonical partial points on the combine stream -> verdict of [8]*sum == 0 (with the
+// bad flag), optional compressed check8 and canonical sum
+static int combine_points(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad, uint8_t check8[32],
+                          uint8_t sum[128]) {
+  Slot& s = ctx->comb;
+  int rc = init_slot(ctx, s);
   if (rc) return rc;
-  Slot& s = ctx->slot[0];
-  if (s.pending) { ctx->err = "slot 0 busy"; return EDC_ERR_ARG; }
-  if (g) CK(hipMemcpyAsync(ctx->aux, partials, g * 128, hipMemcpyHostToDevice, s.st));
+  if (g * 128 > ctx->comb_cap) {
+    if (ctx->comb_in) (void)hipFree(ctx->comb_in);
+    ctx->comb_cap = 0;
+    CK(dalloc(&ctx->comb_in, g * 128 + 1024));
+    ctx->comb_cap = g * 128 + 1024;
+  }
+  if (g) CK(hipMemcpyAsync(ctx->comb_in, partials, g * 128, hipMemcpyHostToDevice, s.st));
   CK(hipMemsetAsync(s.d_out, 0, 256, s.st));
-  launch_combine(s.st, (uint32_t)g, ctx->aux, bad_any ? 1 : 0, check8 != nullptr, s.d_out);
+  launch_combine(s.st, (uint32_t)g, ctx->comb_in, bad ? 1 : 0, check8 != nullptr, s.d_out);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, s.st));
   s.pending = true;
   s.timed = false;
-  return finish_batch(ctx, s, check8, nullptr, nullptr);
+  return finish_batch(ctx, s, check8, sum, nullptr);
+}
+
+int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad_any, uint8_t check8[32]) {
+  if (!ctx || (g && !partials)) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  return combine_points(ctx, g, partials, bad_any, check8, nullptr);
 }
 
 int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
@@ -507,17 +536,7 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
 // sum of g canonical partial points (128-byte records) -> canonical sum, and the verdict of
 // [8]*sum == 0 (with the OR of the bad flags)
 static int sum_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad, uint8_t sum[128]) {
-  int rc = ensure_aux(ctx, g * 128 + 1);
-  if (rc) return rc;
-  Slot& s = ctx->slot[0];
-  CK(hipMemcpyAsync(ctx->aux, partials, g * 128, hipMemcpyHostToDevice, s.st));
-  CK(hipMemsetAsync(s.d_out, 0, 256, s.st));
-  launch_combine(s.st, (uint32_t)g, ctx->aux, bad, 0, s.d_out);
-  CK(hipGetLastError());
-  CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, s.st));
-  s.pending = true;
-  s.timed = false;
-  return finish_batch(ctx, s, nullptr, sum, nullptr);
+  return combine_points(ctx, g, partials, bad, nullptr, sum);
 }
 
 // canonical -P from canonical P (x -> p - x on X and T)
