@@ -12,9 +12,9 @@ using namespace edc;
 namespace {
 
 // phases in enqueue order (each bracketed by HIP events on the slot stream)
-enum Phase { PH_KEYS, PH_CHALLENGE, PH_DECOMP, PH_COEF, PH_MSM_BIN, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
-const char* kPhaseNames[PH_N] = {"keys_group", "challenge_sha512", "decompress_R",
-                                 "coef_chacha_scalar", "msm_bin", "msm_bucket", "msm_window_final"};
+enum Phase { PH_KEYS, PH_CHALLENGE, PH_COEF, PH_MSM_BIN, PH_DECOMP, PH_MSM_BUCKET, PH_MSM_TAIL, PH_N };
+const char* kPhaseNames[PH_N] = {"keys_group", "challenge_sha512", "coef_chacha_scalar", "msm_bin",
+                                 "decompress_R", "msm_bucket", "msm_window_final"};
 
 template <typename T>
 hipError_t dalloc(T** p, size_t count) {
@@ -268,12 +268,14 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   CK(hipEventRecord(s.join, s.side));
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
-  mark(PH_DECOMP);
-  launch_decompress(st, N, d_sig, s.pts, s.flags);
   mark(PH_COEF);
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags);
   mark(PH_MSM_BIN);
   launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  // the R_i are decoded last, right before the accumulation gathers them, so the freshly written
+  // point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
+  mark(PH_DECOMP);
+  launch_decompress(st, N, d_sig, s.pts, s.flags);
   CK(hipStreamWaitEvent(st, s.join, 0));
   mark(PH_MSM_BUCKET);
   launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
