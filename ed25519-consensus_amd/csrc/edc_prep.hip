@@ -35,7 +35,10 @@ __global__ void __launch_bounds__(256, EDC_SHA_WAVES) k_challenge(uint32_t n, co
 }
 
 // ZIP215 decode of every signature's R_i -> points[1 + i] (affine Niels).
-__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
+#ifndef EDC_DEC_WAVES
+#define EDC_DEC_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, EDC_DEC_WAVES) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
                                                        uint32_t* __restrict__ pts, int* __restrict__ flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -1,0 +1,138 @@
+// Where does a field squaring's time go on gfx950? Runs the production fe_sqr as dependent
+// chains under several occupancy / ILP shapes and stamps the in-kernel clock
+// (s_memtime / s_memrealtime, MI355X_MICROARCH.md DVFS item 6), so the cost can be stated in
+// real shader cycles per wave-squaring per SIMD and compared with the instruction-issue sum.
+// Result (profiles/r01_sqr_probe.txt): ~380 cycles per wave-squaring at every occupancy (2-8
+// waves/SIMD) and with two independent chains per lane, so the squaring is VALU-issue-bound;
+// 16 extra `s_nop 0` per squaring cost nothing (the hazard pads LLVM puts after inline asm are
+// free), and a hazard-aware hand schedule of every instruction (tried, not kept) ran the same.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../ed25519-consensus_amd/csrc sqr_probe.hip -o sqr_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include <algorithm>
+#include "fe25519.h"
+using namespace edc;
+
+#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+constexpr int ITERS = 1024;
+
+__device__ fe seed_fe(uint32_t s) {
+  fe a;
+  for (int i = 0; i < 9; ++i) a.v[i] = (s * 2654435761u + i * 40503u) & M29;
+  return a;
+}
+
+__device__ __forceinline__ void stamp(unsigned long long* clk, uint64_t t0, uint64_t r0) {
+  if (threadIdx.x == 0) {
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    clk[2 * blockIdx.x] = t1 - t0;
+    clk[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, W) k_sqr(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe a = seed_fe(s + blockIdx.x * 256 + threadIdx.x);
+  for (int i = 0; i < ITERS; ++i) a = fe_sqr(a);
+  out[blockIdx.x * 256 + threadIdx.x] = a.v[0] ^ a.v[8];
+  stamp(clk, t0, r0);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, W) k_sqr2(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe a = seed_fe(s + blockIdx.x * 256 + threadIdx.x), b = seed_fe(s * 3 + blockIdx.x * 256 + threadIdx.x);
+  for (int i = 0; i < ITERS / 2; ++i) { a = fe_sqr(a); b = fe_sqr(b); }
+  out[blockIdx.x * 256 + threadIdx.x] = a.v[0] ^ a.v[8] ^ b.v[1];
+  stamp(clk, t0, r0);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, W) k_mul(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe a = seed_fe(s + blockIdx.x * 256 + threadIdx.x), b = seed_fe(s * 7 + threadIdx.x);
+  for (int i = 0; i < ITERS; ++i) a = fe_mul(a, b);
+  out[blockIdx.x * 256 + threadIdx.x] = a.v[0] ^ a.v[8];
+  stamp(clk, t0, r0);
+}
+
+// pure issue rate of independent v_mad_u64_u32 (8 chains), for the cycle calibration
+template <int W>
+__global__ void __launch_bounds__(256, W) k_mad(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t acc[8];
+  uint32_t x = s + threadIdx.x, y = s ^ blockIdx.x;
+  for (int j = 0; j < 8; ++j) acc[j] = j;
+  for (int i = 0; i < ITERS * 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = mad64(x + j, y, acc[j]);
+  uint64_t r = 0;
+  for (int j = 0; j < 8; ++j) r ^= acc[j];
+  out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)r ^ (uint32_t)(r >> 32);
+  stamp(clk, t0, r0);
+}
+
+// price of s_nop 0: the production squaring plus 16 explicit pads
+template <int W>
+__global__ void __launch_bounds__(256, W) k_sqr_nop(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe a = seed_fe(s + blockIdx.x * 256 + threadIdx.x);
+  for (int i = 0; i < ITERS; ++i) {
+    a = fe_sqr(a);
+    asm volatile("s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n"
+                 "s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0");
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = a.v[0] ^ a.v[8];
+  stamp(clk, t0, r0);
+}
+
+typedef void (*kfn)(uint32_t*, unsigned long long*, uint32_t);
+
+// occupancy is pinned with dynamic LDS: w blocks of 256 lanes (one wave per SIMD each) per CU
+int run(const char* name, kfn f, int w, double ops_per_lane, double issue_est, uint32_t* d, unsigned long long* clk, int blocks) {
+  const size_t lds = (160 * 1024) / w - 1024;
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+  for (int r = 0; r < 20; ++r) hipLaunchKernelGGL(f, dim3(blocks), dim3(256), lds, 0, d, clk, 1u + r);  // warm the clock state
+  CHK(hipDeviceSynchronize());
+  const int reps = 10;
+  CHK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(f, dim3(blocks), dim3(256), lds, 0, d, clk, 100u + r);
+  CHK(hipEventRecord(e1));
+  CHK(hipEventSynchronize(e1));
+  float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> h(2 * blocks);
+  CHK(hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<double> ghz;
+  for (int b = 0; b < blocks; ++b) if (h[2 * b + 1]) ghz.push_back((double)h[2 * b] / h[2 * b + 1] * 0.1);
+  std::sort(ghz.begin(), ghz.end());
+  double clk_ghz = ghz[ghz.size() / 2];
+  double lane_ops = (double)blocks * 256 * ops_per_lane * reps;
+  double wave_ops_per_simd = lane_ops / 64 / 1024;
+  double cyc = ms * 1e-3 * clk_ghz * 1e9 / wave_ops_per_simd;
+  printf("%-14s %8.3f ms  %7.2f G lane-ops/s  clock %.3f GHz  %7.1f cyc/wave-op/SIMD  (issue estimate %.0f)\n", name,
+         ms / reps, lane_ops / (ms * 1e-3) / 1e9, clk_ghz, cyc, issue_est);
+  return 0;
+}
+
+int main() {
+  const int blocks = 256 * 8 * 4;
+  uint32_t* d;
+  unsigned long long* clk;
+  CHK(hipMalloc(&d, (size_t)blocks * 256 * 4));
+  CHK(hipMalloc(&clk, (size_t)blocks * 16));
+  run("mad x8 w4", k_mad<4>, 4, ITERS * 8 * 8, 4, d, clk, blocks);
+  run("mad x8 w8", k_mad<8>, 8, ITERS * 8 * 8, 4, d, clk, blocks);
+  run("sqr w4", k_sqr<4>, 4, ITERS, 336, d, clk, blocks);
+  run("sqr w8", k_sqr<8>, 8, ITERS, 336, d, clk, blocks);
+  run("sqr ilp2 w4", k_sqr2<4>, 4, ITERS, 336, d, clk, blocks);
+  run("sqr ilp2 w2", k_sqr2<2>, 2, ITERS, 336, d, clk, blocks);
+  run("sqr+16nop w4", k_sqr_nop<4>, 4, ITERS, 336, d, clk, blocks);
+  run("mul w4", k_mul<4>, 4, ITERS, 456, d, clk, blocks);
+  run("mul w8", k_mul<8>, 8, ITERS, 456, d, clk, blocks);
+  CHK(hipFree(d));
+  return 0;
+}
