@@ -41,7 +41,7 @@ ABI_SYMBOLS = [
     "edc_batch_submit_device", "edc_batch_wait", "edc_verify_each", "edc_verify_each_device",
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
-    "edc_synchronize",
+    "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
 ]
 
 
@@ -120,6 +120,12 @@ def load_library(path=None):
         lib.edc_timing_name.restype = ctypes.c_char_p
         lib.edc_timing_name.argtypes = [ctypes.c_int]
         lib.edc_synchronize.argtypes = [c_vp]
+        lib.edc_vk_validate.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+        lib.edc_keycache_load.restype = ctypes.c_int64
+        lib.edc_keycache_load.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+        lib.edc_keycache_clear.argtypes = [c_vp]
+        lib.edc_keycache_size.restype = c_sz
+        lib.edc_keycache_size.argtypes = [c_vp]
         if path is None:
             _lib = lib
         return lib
@@ -229,6 +235,30 @@ class Engine:
         with self._lock:
             self._check(self.lib.edc_decompress(self.ctx, n, b"".join(encs) or b"\0", xy, ok))
         return [(bool(ok.raw[i]), xy.raw[64 * i:64 * i + 32], xy.raw[64 * i + 32:64 * i + 64]) for i in range(n)]
+
+    def vk_validate(self, encs):
+        """VerificationKey::try_from for many keys (src/verification_key.rs:160-175): codes 0 / 2."""
+        n = len(encs)
+        out = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            self._check(self.lib.edc_vk_validate(self.ctx, n, b"".join(encs) or b"\0", out))
+        return list(out.raw[:n])
+
+    def keycache_load(self, encs):
+        """Register validator keys (decoded once per context, comb tables kept on the GPU).
+        Returns (number of distinct keys cached, per-key ok list)."""
+        n = len(encs)
+        ok = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            u = self._check(self.lib.edc_keycache_load(self.ctx, n, b"".join(encs) or b"\0", ok))
+        return u, [bool(b) for b in ok.raw[:n]]
+
+    def keycache_clear(self):
+        with self._lock:
+            self._check(self.lib.edc_keycache_clear(self.ctx))
+
+    def keycache_size(self):
+        return int(self.lib.edc_keycache_size(self.ctx))
 
     def sign(self, seeds, msgs, seed_index=None):
         n = len(msgs)
@@ -340,10 +370,17 @@ class VerificationKey:
     def try_from(cls, data, engine=None):
         vkb = data if isinstance(data, VerificationKeyBytes) else VerificationKeyBytes(data)
         eng = engine or default_engine()
-        ok, _, _ = eng.decompress([vkb.to_bytes()])[0]
-        if not ok:
+        if eng.vk_validate([vkb.to_bytes()])[0] != EDC_OK:
             raise MalformedPublicKey()
         return cls(vkb, eng)
+
+    @classmethod
+    def try_from_many(cls, keys, engine=None):
+        """Batched key ingestion: [VerificationKey or MalformedPublicKey()] per input, one launch."""
+        vkbs = [k if isinstance(k, VerificationKeyBytes) else VerificationKeyBytes(k) for k in keys]
+        eng = engine or default_engine()
+        codes = eng.vk_validate([v.to_bytes() for v in vkbs])
+        return [cls(v, eng) if c == EDC_OK else MalformedPublicKey() for v, c in zip(vkbs, codes)]
 
     def to_bytes(self):
         return self.A_bytes.to_bytes()

@@ -2,6 +2,7 @@
 // Every entry point cites the reference API it replaces in include/edc.h.
 #include <string.h>
 #include <string>
+#include <unordered_map>
 #include <vector>
 #include "edc.h"
 #include "edc_common.h"
@@ -73,7 +74,16 @@ struct edc_ctx {
   float last_ms[PH_N] = {};
   int nlast = 0;
   int64_t next_ticket = 0;
+  // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
+  uint32_t *kc_table = nullptr, *kc_keys = nullptr, *kc_comb = nullptr;
+  uint8_t* kc_ok = nullptr;
+  uint32_t* bcomb = nullptr;    // comb table of B, built with the first cache
+  uint32_t kc_m = 0, kc_tmask = 0;
   hipStream_t st() const { return slot[0].st; }
+  KeyCacheView kc() const {
+    if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0};
+    return KeyCacheView{kc_table, kc_keys, kc_ok, kc_comb, kc_tmask, kc_m};
+  }
 };
 
 #define CK(expr)                                                        \
@@ -264,7 +274,8 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   // reads them
   CK(hipEventRecord(s.fork, st));
   CK(hipStreamWaitEvent(s.side, s.fork, 0));
-  launch_key_points(s.side, N, d_vk, s.key_rep, s.pts, ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags);
+  launch_key_points(s.side, N, d_vk, s.key_rep, s.pts, ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags,
+                    ctx->kc());
   CK(hipEventRecord(s.join, s.side));
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
@@ -343,9 +354,29 @@ edc_ctx* edc_create(int device) {
   return ctx;
 }
 
+static void free_keycache(edc_ctx* ctx) {
+  void* ptrs[] = {ctx->kc_table, ctx->kc_keys, ctx->kc_comb, ctx->kc_ok};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  ctx->kc_table = ctx->kc_keys = ctx->kc_comb = nullptr;
+  ctx->kc_ok = nullptr;
+  ctx->kc_m = ctx->kc_tmask = 0;
+}
+
+static int sync_all(edc_ctx* ctx) {
+  for (Slot& s : ctx->slot) {
+    if (s.st) CK(hipStreamSynchronize(s.st));
+    if (s.side) CK(hipStreamSynchronize(s.side));
+  }
+  return 0;
+}
+
 void edc_destroy(edc_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  (void)sync_all(ctx);
+  free_keycache(ctx);
+  if (ctx->bcomb) (void)hipFree(ctx->bcomb);
   for (Slot& s : ctx->slot) {
     if (s.st) (void)hipStreamSynchronize(s.st);
     free_slot_buffers(s);
@@ -496,7 +527,8 @@ int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const u
   CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->kbuf, k, n * 32, hipMemcpyHostToDevice, st));
-  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts);
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts,
+                       ctx->kc(), ctx->bcomb);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
@@ -512,7 +544,8 @@ int edc_verify_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* si
   if (!n) return 0;
   hipStream_t st = ctx->st();
   launch_challenge(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->msg, ctx->off, ctx->kbuf);
-  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts);
+  launch_verify_single(st, (uint32_t)n, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts,
+                       ctx->kc(), ctx->bcomb);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(verdicts, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
@@ -528,7 +561,8 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
   if (!n) return 0;
   hipStream_t st = ctx->st();
   launch_challenge(st, (uint32_t)n, d_vk, d_sig, d_msg, d_msg_off, ctx->kbuf);
-  launch_verify_single(st, (uint32_t)n, d_vk, d_sig, ctx->kbuf, ctx->btab, ctx->vtab, d_verdicts);
+  launch_verify_single(st, (uint32_t)n, d_vk, d_sig, ctx->kbuf, ctx->btab, ctx->vtab, d_verdicts,
+                       ctx->kc(), ctx->bcomb);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));
   return 0;
@@ -591,7 +625,8 @@ int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
       hipStream_t st = ctx->st();
       launch_challenge(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, d_msg, d_msg_off + nd.lo, ctx->kbuf);
       launch_verify_single(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, ctx->kbuf, ctx->btab, ctx->vtab,
-                           ctx->verdicts);
+                           ctx->verdicts,
+                       ctx->kc(), ctx->bcomb);
       CK(hipGetLastError());
       CK(hipMemcpyAsync(verdicts + nd.lo, ctx->verdicts, m, hipMemcpyDeviceToHost, st));
       CK(hipStreamSynchronize(st));
@@ -637,6 +672,90 @@ int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint
   CK(hipMemcpyAsync(ok, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
   return 0;
+}
+
+int edc_vk_validate(edc_ctx* ctx, size_t n, const uint8_t* vk, uint8_t* codes) {
+  if (!ctx || (n && (!vk || !codes))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  int rc = ensure_n(ctx, n);
+  if (rc) return rc;
+  if (!n) return 0;
+  hipStream_t st = ctx->st();
+  CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
+  launch_vk_validate(st, (uint32_t)n, ctx->vk, ctx->verdicts);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(codes, ctx->verdicts, n, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int edc_keycache_clear(edc_ctx* ctx) {
+  if (!ctx) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  for (Slot& s : ctx->slot)
+    if (s.pending) { ctx->err = "key cache change with a batch in flight"; return EDC_ERR_ARG; }
+  int rc = sync_all(ctx);
+  if (rc) return rc;
+  free_keycache(ctx);
+  return 0;
+}
+
+size_t edc_keycache_size(const edc_ctx* ctx) { return ctx ? ctx->kc_m : 0; }
+
+int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok) {
+  if (!ctx || (m && !vk)) return EDC_ERR_ARG;
+  int rc = edc_keycache_clear(ctx);
+  if (rc) return rc;
+  if (!m) return 0;
+  // distinct keys in first-occurrence order (the cache is keyed on raw bytes, like the batch's
+  // HashMap<VerificationKeyBytes, _>, src/batch.rs:114)
+  std::unordered_map<std::string, uint32_t> idx;
+  std::vector<uint32_t> of(m), words;
+  for (size_t i = 0; i < m; ++i) {
+    auto it = idx.emplace(std::string(reinterpret_cast<const char*>(vk + 32 * i), 32), (uint32_t)idx.size());
+    of[i] = it.first->second;
+    if (it.second) {
+      if (idx.size() > KC_MAX_KEYS) { ctx->err = "key cache holds at most 65536 keys"; return EDC_ERR_ARG; }
+      uint32_t w[8];
+      memcpy(w, vk + 32 * i, 32);
+      words.insert(words.end(), w, w + 8);
+    }
+  }
+  const uint32_t u = (uint32_t)idx.size();
+  const uint32_t T = (uint32_t)next_pow2(2 * (size_t)(u < 8 ? 8 : u));
+  std::vector<uint32_t> table(T, KC_EMPTY);
+  for (uint32_t c = 0; c < u; ++c) {
+    uint32_t h = kc_hash(&words[8 * c]) & (T - 1);
+    while (table[h] != KC_EMPTY) h = (h + 1) & (T - 1);
+    table[h] = c;
+  }
+  uint32_t* ext = nullptr;
+  CK(dalloc(&ctx->kc_table, T));
+  CK(dalloc(&ctx->kc_keys, (size_t)u * 8));
+  CK(dalloc(&ctx->kc_ok, u));
+  CK(dalloc(&ctx->kc_comb, (size_t)u * COMB_ENTRIES * NIELS_WORDS));
+  CK(dalloc(&ext, (size_t)(u + 1) * EXT_WORDS));
+  hipStream_t st = ctx->st();
+  CK(hipMemcpyAsync(ctx->kc_table, table.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(ctx->kc_keys, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  launch_kc_decode(st, u, ctx->kc_keys, ext, ctx->kc_ok);
+  launch_kc_comb(st, u, ext, ctx->kc_comb);
+  if (!ctx->bcomb) {
+    CK(dalloc(&ctx->bcomb, (size_t)COMB_ENTRIES * NIELS_WORDS));
+    uint32_t* bext = ext + (size_t)u * EXT_WORDS;
+    launch_kc_basepoint(st, bext);
+    launch_kc_comb(st, 1, bext, ctx->bcomb);
+  }
+  CK(hipGetLastError());
+  std::vector<uint8_t> uok(u);
+  CK(hipMemcpyAsync(uok.data(), ctx->kc_ok, u, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  (void)hipFree(ext);
+  ctx->kc_m = u;
+  ctx->kc_tmask = T - 1;
+  if (ok)
+    for (size_t i = 0; i < m; ++i) ok[i] = uok[of[i]];
+  return u;
 }
 
 int edc_sign_device(edc_ctx* ctx, size_t n, const uint8_t* d_seeds, const uint32_t* d_seed_index,

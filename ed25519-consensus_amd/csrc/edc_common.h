@@ -7,6 +7,7 @@
 #include "sc25519.h"
 #include "sha512.h"
 #include "chacha20.h"
+#include "keycache.h"
 
 namespace edc {
 

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "keycache.h"
 
 namespace edc {
 // edc_prep.hip
@@ -9,7 +10,7 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
 void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags);
+                       const uint32_t* bshift, int* flags, const KeyCacheView& kc);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
                  uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
@@ -32,7 +33,14 @@ size_t msm_entry_capacity(uint32_t n);
 // edc_single.hip
 void launch_init_btable(hipStream_t st, uint32_t* btab);
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
-                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict);
+                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict,
+                          const KeyCacheView& kc, const uint32_t* bcomb);
+// key cache (edc_single.hip): decode m registered keys -> ext + ok, comb tables of m points
+void launch_kc_decode(hipStream_t st, uint32_t m, const uint32_t* keys, uint32_t* ext, uint8_t* ok);
+void launch_kc_basepoint(hipStream_t st, uint32_t* ext);
+void launch_kc_comb(hipStream_t st, uint32_t m, const uint32_t* ext, uint32_t* comb);
+// VerificationKey::try_from for n encodings: code[i] = 0 (Ok) or 2 (MalformedPublicKey)
+void launch_vk_validate(hipStream_t st, uint32_t n, const uint8_t* enc, uint8_t* code);
 size_t verify_single_scratch_words(size_t n);
 void launch_sign(hipStream_t st, uint32_t n, const uint8_t* seeds, const uint32_t* seed_index,
                  const uint8_t* msg, const uint64_t* off, const uint32_t* btab, uint8_t* vk_out,

@@ -50,15 +50,30 @@ __global__ void __launch_bounds__(256, EDC_DEC_WAVES) k_decompress(uint32_t n, c
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
 
+// one 128-byte Niels record src -> pts[idx]
+__device__ __forceinline__ void copy_record(uint32_t* __restrict__ pts, uint32_t idx, const uint32_t* __restrict__ src) {
+  const uint4* q = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(pts + (size_t)idx * NIELS_WORDS);
+#pragma unroll
+  for (int i = 0; i < NIELS_WORDS / 4; ++i) d[i] = q[i];
+}
+
 // Side stream, concurrent with k_decompress: ZIP215 decode of each distinct key j (its first
 // signature's raw bytes, src/batch.rs:183-185) -> points[1 + n + j].
 __global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep,
-                                                       uint32_t* __restrict__ pts, int* __restrict__ flags) {
+                                                       uint32_t* __restrict__ pts, int* __restrict__ flags,
+                                                       KeyCacheView kcache) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
   uint32_t w[8];
   ld_words8(vk + (size_t)key_rep[j] * 32, w);
+  const int ci = kc_lookup(kcache, w);
+  if (ci >= 0) {                    // registered key: A = comb[0][0], decoded once per context
+    copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
+    if (!kcache.ok[ci]) atomicOr(&flags[FLAG_BAD], 1);
+    return;
+  }
   ge_p3 P;
   const bool ok = ge_decompress(w, P);
   st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
@@ -74,15 +89,26 @@ __device__ __forceinline__ fe fe_inv2() {
 // Few-key mode only (side stream, after k_key_points): [2^128]A_j as affine Niels at
 // points[1 + n + m + j], one quad of lanes per key (quad-cooperative doublings, ge_quad.h), and
 // the context constant [2^128]B copied to points[n + 2m + 1].
-__global__ void __launch_bounds__(64) k_key_shift(uint32_t n, uint32_t* __restrict__ pts,
+__global__ void __launch_bounds__(64) k_key_shift(uint32_t n, const uint8_t* __restrict__ vk,
+                                                  const uint32_t* __restrict__ key_rep, uint32_t* __restrict__ pts,
                                                   const uint32_t* __restrict__ bshift,
-                                                  const int* __restrict__ flags) {
+                                                  const int* __restrict__ flags, KeyCacheView kcache) {
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   if (!few_key_mode(n, m)) return;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < NIELS_WORDS) pts[(size_t)(n + 2 * m + 1) * NIELS_WORDS + t] = bshift[t];
   const uint32_t j = t >> 2;          // whole quads share j: a quad is active or exits together
   if (j >= m) return;
+  if (kcache.table) {                 // registered key: [2^128]A = comb[32][0]
+    uint32_t w[8];
+    ld_words8(vk + (size_t)key_rep[j] * 32, w);
+    const int ci = kc_lookup(kcache, w);
+    if (ci >= 0) {
+      if ((t & 3) == 0)
+        copy_record(pts, 1 + n + m + j, kcache.comb + ((size_t)ci * COMB_ENTRIES + COMB_SHIFT128) * NIELS_WORDS);
+      return;
+    }
+  }
   const ge_niels a = ld_niels(pts, 1 + n + j);
   ge_p3 P;
   P.X = fe_mul(fe_sub(a.ypx, a.ymx), fe_inv2());
@@ -356,14 +382,14 @@ void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t*
   if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
 }
 void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags) {
+                       const uint32_t* bshift, int* flags, const KeyCacheView& kc) {
   if (!n) return;
   // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
   // on the device and surplus blocks exit at once
-  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags);
+  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
   if (n >= FEW_KEY_MIN_N)
     hipLaunchKernelGGL(k_key_shift, dim3(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64)), dim3(64), 0, st, n,
-                       pts, bshift, flags);
+                       vk, key_rep, pts, bshift, flags, kc);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,

@@ -118,16 +118,70 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
 }
 
 // verdict codes: 0 Ok, 1 InvalidSignature, 2 MalformedPublicKey
+// Cached key (keycache.h): [s]B - [k]A from the key's and B's comb tables, 64 positions of
+// signed radix-16 digits, one affine Niels record per digit and NO doublings (the joint
+// windowed loop below needs 252). Zero digits add the identity (branch-free across the wave).
+__device__ ge_p3 comb_double_base(const uint32_t k[8], const uint32_t s[8], const uint32_t* __restrict__ acomb,
+                                  const uint32_t* __restrict__ bcomb) {
+  const uint64_t kc = radix16_carries(k), sc = radix16_carries(s);
+  ge_p3 acc = ge_identity();
+  for (int j = 0; j < COMB_POS; ++j) {
+    const int a = radix16_digit(k, kc, j);
+    const int ai = a < 0 ? -a : a;
+    ge_niels q = ai ? ld_niels(acomb, j * COMB_MULT + ai - 1) : ge_niels_identity();
+    if (a > 0) q = ge_niels_neg(q);            // -[k]A
+    acc = ge_madd(acc, q);
+    EDC_SCHED_FENCE();
+    const int b = radix16_digit(s, sc, j);
+    const int bi = b < 0 ? -b : b;
+    ge_niels nb = bi ? ld_niels(bcomb, j * COMB_MULT + bi - 1) : ge_niels_identity();
+    if (b < 0) nb = ge_niels_neg(nb);
+    acc = ge_madd(acc, nb);
+  }
+  return acc;
+}
+
+// Per-item verification of the items whose key is registered in the context's cache (the
+// other lanes exit; k_verify_single skips these items). Its own kernel, so that neither path
+// inherits the other's register allocation.
+__global__ void __launch_bounds__(SV_THREADS, 3) k_verify_comb(uint32_t n, const uint8_t* __restrict__ vk,
+                                                               const uint8_t* __restrict__ sig,
+                                                               const uint32_t* __restrict__ kscal,
+                                                               uint8_t* __restrict__ verdict, KeyCacheView kcache,
+                                                               const uint32_t* __restrict__ bcomb) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  ld_words8(vk + (size_t)i * 32, w);
+  const int ci = kc_lookup(kcache, w);
+  if (ci < 0) return;
+  if (!kcache.ok[ci]) { verdict[i] = 2; return; }                 // try_from: MalformedPublicKey
+  uint32_t sw[8];
+  ld_words8(sig + (size_t)i * 64 + 32, sw);
+  if (!sc_is_canonical(sw)) { verdict[i] = 1; return; }          // s checked before R
+  uint32_t rw[8];
+  ld_words8(sig + (size_t)i * 64, rw);
+  ge_p3 R;
+  if (!ge_decompress(rw, R)) { verdict[i] = 1; return; }
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  const ge_p3 Rp = comb_double_base(k, sw, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS, bcomb);
+  verdict[i] = ge_is_identity(ge_mul_by_cofactor(ge_add(R, ge_neg(Rp)))) ? 0 : 1;
+}
+
 __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_single(uint32_t n, const uint8_t* __restrict__ vk,
                                                                  const uint8_t* __restrict__ sig,
                                                                  const uint32_t* __restrict__ kscal,
                                                                  const uint32_t* __restrict__ btab,
                                                                  uint32_t* __restrict__ vtab,
-                                                                 uint8_t* __restrict__ verdict) {
+                                                                 uint8_t* __restrict__ verdict,
+                                                                 KeyCacheView kcache) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
   ld_words8(vk + (size_t)i * 32, w);
+  if (kc_lookup(kcache, w) >= 0) return;                          // done by k_verify_comb
   ge_p3 A;
   if (!ge_decompress(w, A)) { verdict[i] = 2; return; }          // try_from: MalformedPublicKey
   uint32_t sw[8];
@@ -240,6 +294,48 @@ __global__ void __launch_bounds__(256) k_decode(uint32_t n, const uint8_t* __res
   words_to_bytes32(wy, xy + (size_t)i * 64 + 32);
 }
 
+// ---- validator-key cache (keycache.h) ----
+__global__ void __launch_bounds__(256) k_kc_decode(uint32_t m, const uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ ext, uint8_t* __restrict__ ok) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  uint32_t w[8];
+  ld_words8(reinterpret_cast<const uint8_t*>(keys + (size_t)i * 8), w);
+  ge_p3 P;
+  ok[i] = ge_decompress(w, P) ? 1 : 0;
+  st_ext(ext + (size_t)i * EXT_WORDS, P);
+}
+
+__global__ void k_kc_basepoint(uint32_t* ext) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) st_ext(ext, ge_basepoint());
+}
+
+// comb[c][j][d-1] = [d 16^j] P_c: one lane per (point, position, multiple), one-off per cache load
+__global__ void __launch_bounds__(256) k_kc_comb(uint32_t m, const uint32_t* __restrict__ ext,
+                                                 uint32_t* __restrict__ comb) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = (uint32_t)(t / COMB_ENTRIES);
+  if (c >= m) return;
+  const uint32_t r = (uint32_t)(t % COMB_ENTRIES);
+  const int j = (int)(r / COMB_MULT), d = (int)(r % COMB_MULT) + 1;
+  ge_p3 P = ld_ext(ext + (size_t)c * EXT_WORDS);
+  for (int q = 0; q < 4 * j; ++q) P = ge_dbl(P);
+  ge_p3 Q = P;
+  for (int q = 1; q < d; ++q) Q = ge_add(Q, P);
+  st_niels(comb + (size_t)c * COMB_ENTRIES * NIELS_WORDS, r, to_niels(Q));
+}
+
+// VerificationKey::try_from (src/verification_key.rs:160-175): 0 Ok, 2 MalformedPublicKey
+__global__ void __launch_bounds__(256) k_vk_validate(uint32_t n, const uint8_t* __restrict__ enc,
+                                                     uint8_t* __restrict__ code) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  ld_words8(enc + (size_t)i * 32, w);
+  ge_p3 P;
+  code[i] = ge_decompress(w, P) ? 0 : 2;
+}
+
 // ChaCha20 keystream bytes [byte_off, byte_off + len) for synthetic data (64-byte aligned start)
 __global__ void __launch_bounds__(256) k_chacha_fill(uint64_t nblocks, uint64_t blk0, uint32_t k0,
                                                      uint32_t k1, uint32_t k2, uint32_t k3, uint32_t k4,
@@ -260,10 +356,26 @@ void launch_init_btable(hipStream_t st, uint32_t* btab) {
   hipLaunchKernelGGL(k_init_btable, dim3(1), dim3(64), 0, st, btab);
 }
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
-                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict) {
+                          const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict,
+                          const KeyCacheView& kc, const uint32_t* bcomb) {
   if (!n) return;
+  if (kc.table)
+    hipLaunchKernelGGL(k_verify_comb, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, verdict, kc,
+                       bcomb);
   hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, btab,
-                     vtab, verdict);
+                     vtab, verdict, kc);
+}
+void launch_kc_decode(hipStream_t st, uint32_t m, const uint32_t* keys, uint32_t* ext, uint8_t* ok) {
+  if (m) hipLaunchKernelGGL(k_kc_decode, dim3(cdiv(m, 256)), dim3(256), 0, st, m, keys, ext, ok);
+}
+void launch_kc_basepoint(hipStream_t st, uint32_t* ext) {
+  hipLaunchKernelGGL(k_kc_basepoint, dim3(1), dim3(64), 0, st, ext);
+}
+void launch_kc_comb(hipStream_t st, uint32_t m, const uint32_t* ext, uint32_t* comb) {
+  if (m) hipLaunchKernelGGL(k_kc_comb, dim3(cdiv((uint64_t)m * COMB_ENTRIES, 256)), dim3(256), 0, st, m, ext, comb);
+}
+void launch_vk_validate(hipStream_t st, uint32_t n, const uint8_t* enc, uint8_t* code) {
+  if (n) hipLaunchKernelGGL(k_vk_validate, dim3(cdiv(n, 256)), dim3(256), 0, st, n, enc, code);
 }
 size_t verify_single_scratch_words(size_t n) { return n * SV_TAB_WORDS; }
 void launch_sign(hipStream_t st, uint32_t n, const uint8_t* seeds, const uint32_t* seed_index,

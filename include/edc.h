@@ -153,6 +153,29 @@ int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
 int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok);
 
 /*
+ * VerificationKey::try_from(VerificationKeyBytes) for n keys at once -- key ingestion, e.g. a
+ * validator set or serde-deserialized keys (reference src/verification_key.rs:160-175, :106-109;
+ * tests/unit_tests.rs:32-40). codes[i] = EDC_OK or EDC_MALFORMED_PUBLIC_KEY. Returns 0 or <0.
+ */
+int edc_vk_validate(edc_ctx* ctx, size_t n, const uint8_t* vk, uint8_t* codes);
+
+/*
+ * Persistent validator-key cache: the reference's VerificationKey keeps its decoded point
+ * (src/verification_key.rs:106-114, :160-175) while batch::Verifier re-decodes every distinct
+ * key per verify (src/batch.rs:183-185). edc_keycache_load decodes the m keys (n*32 bytes,
+ * duplicates allowed) ONCE and keeps a 64 KB fixed-base table per distinct key in this
+ * context, replacing any previous cache. Every later batch / per-item call on the context
+ * takes A and [2^128]A of a registered key from the cache, and the per-item fallback computes
+ * [s]B - [k]A for it without doublings. Verdicts are identical with and without the cache
+ * (an undecodable registered key stays MalformedPublicKey / fails the batch). ok (nullable,
+ * m bytes) receives 1 where the key decodes. Returns the number of distinct keys cached
+ * (<= 65536) or <0; refused while submitted batches are in flight.
+ */
+int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok);
+int edc_keycache_clear(edc_ctx* ctx);
+size_t edc_keycache_size(const edc_ctx* ctx);
+
+/*
  * SigningKey::from([u8;32]) + SigningKey::sign (reference src/signing_key.rs:118-150,
  * :186-205) -- test/benchmark data source. seed_index (nullable) maps item i to seed
  * seed_index[i] (shared validator keys); vk_out n*32, sig_out n*64.

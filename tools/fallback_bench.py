@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--keys", type=int, default=150)
     ap.add_argument("--msg-len", type=int, default=120)
     ap.add_argument("--leaf", type=int, default=65536)
+    ap.add_argument("--leaf-cached", type=int, default=0, help="grouped-fallback leaf with the key cache")
     args = ap.parse_args()
     import torch
     import bench
@@ -65,9 +66,31 @@ def main():
     nbad, t_group = timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, args.leaf, verdicts))
     flagged_group = [i for i, c in enumerate(verdicts.raw) if c]
     assert flagged_each == flagged_group == [bad], (flagged_each[:5], flagged_group[:5], bad)
-    print(json.dumps({"n": n, "validators": args.keys, "bad_index": bad, "batch_ms": round(t_batch, 3),
-                      "per_sig_fallback_ms": round(t_each, 3), "grouped_fallback_ms": round(t_group, 3),
-                      "leaf": args.leaf, "per_sig_sigs_per_s": round(n / t_each * 1e3, 1)}))
+    out = {"n": n, "validators": args.keys, "bad_index": bad, "batch_ms": round(t_batch, 3),
+           "per_sig_fallback_ms": round(t_each, 3), "grouped_fallback_ms": round(t_group, 3),
+           "leaf": args.leaf, "per_sig_sigs_per_s": round(n / t_each * 1e3, 1)}
+    if args.keys:
+        # the same three with the validator keys registered in the context's key cache
+        keys = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
+        t0 = time.perf_counter()
+        u, ok = eng.keycache_load([keys[32 * i:32 * i + 32] for i in range(len(keys) // 32)])
+        t_load = (time.perf_counter() - t0) * 1e3
+        assert all(ok)
+        timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
+        rc, t_batch_c = timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
+        assert rc == 1
+        ver.zero_()
+        timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
+        _, t_each_c = timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
+        assert torch.nonzero(ver).flatten().tolist() == [bad]
+        leaf_c = args.leaf_cached or args.leaf
+        timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, leaf_c, verdicts))
+        nbad, t_group_c = timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, leaf_c, verdicts))
+        assert [i for i, c in enumerate(verdicts.raw) if c] == [bad]
+        out["keycache"] = {"keys": u, "load_ms": round(t_load, 3), "batch_ms": round(t_batch_c, 3),
+                           "per_sig_fallback_ms": round(t_each_c, 3), "grouped_fallback_ms": round(t_group_c, 3),
+                           "leaf": leaf_c, "per_sig_sigs_per_s": round(n / t_each_c * 1e3, 1)}
+    print(json.dumps(out))
     eng.close()
 
 
