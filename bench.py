@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight per GPU (submit/wait pipelining)")
+    ap.add_argument("--keycache", action="store_true",
+                    help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
     ap.add_argument("--probe", action="store_true", help="measurement-probe builds: do not require Ok verdicts")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -202,6 +204,9 @@ def main():
             codes.append(wait_oldest())
         return codes
 
+    if args.keycache and args.keys > 0:           # a node's known validator set, registered once
+        kb = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
+        eng.keycache_load([kb[32 * i:32 * i + 32] for i in range(len(kb) // 32)])
     eng._check(lib.edc_reserve(eng.ctx, n))        # both in-flight slots' workspaces, before any step
     run_steps(args.warmup)
     if dist:
@@ -271,7 +276,7 @@ def main():
             "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
             "config": {"workload": c_desc,
                        "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
-                       "inflight": args.inflight,
+                       "inflight": args.inflight, "keycache": bool(args.keycache and args.keys > 0),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

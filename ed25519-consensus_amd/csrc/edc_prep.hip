@@ -64,20 +64,23 @@ __global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t
                                                        const uint32_t* __restrict__ key_rep,
                                                        uint32_t* __restrict__ pts, int* __restrict__ flags,
                                                        KeyCacheView kcache) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
-  uint32_t w[8];
-  ld_words8(vk + (size_t)key_rep[j] * 32, w);
-  const int ci = kc_lookup(kcache, w);
-  if (ci >= 0) {                    // registered key: A = comb[0][0], decoded once per context
-    copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
-    if (!kcache.ok[ci]) atomicOr(&flags[FLAG_BAD], 1);
-    return;
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  // grid-stride: the grid is sized for the largest possible m, but capped, so a few-key batch
+  // does not dispatch thousands of waves that only read m and exit
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+    uint32_t w[8];
+    ld_words8(vk + (size_t)key_rep[j] * 32, w);
+    const int ci = kc_lookup(kcache, w);
+    if (ci >= 0) {                  // registered key: A = comb[0][0], decoded once per context
+      copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
+      if (!kcache.ok[ci]) atomicOr(&flags[FLAG_BAD], 1);
+      continue;
+    }
+    ge_p3 P;
+    const bool ok = ge_decompress(w, P);
+    st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
+    if (!ok) atomicOr(&flags[FLAG_BAD], 1);
   }
-  ge_p3 P;
-  const bool ok = ge_decompress(w, P);
-  st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
-  if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
 
 // 1/2 mod p: affine (x, y) back from a Niels record, x = (ypx - ymx)/2, y = (ypx + ymx)/2
@@ -95,34 +98,36 @@ __global__ void __launch_bounds__(64) k_key_shift(uint32_t n, const uint8_t* __r
                                                   const int* __restrict__ flags, KeyCacheView kcache) {
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   if (!few_key_mode(n, m)) return;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < NIELS_WORDS) pts[(size_t)(n + 2 * m + 1) * NIELS_WORDS + t] = bshift[t];
-  const uint32_t j = t >> 2;          // whole quads share j: a quad is active or exits together
-  if (j >= m) return;
-  if (kcache.table) {                 // registered key: [2^128]A = comb[32][0]
-    uint32_t w[8];
-    ld_words8(vk + (size_t)key_rep[j] * 32, w);
-    const int ci = kc_lookup(kcache, w);
-    if (ci >= 0) {
-      if ((t & 3) == 0)
-        copy_record(pts, 1 + n + m + j, kcache.comb + ((size_t)ci * COMB_ENTRIES + COMB_SHIFT128) * NIELS_WORDS);
-      return;
+  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 < NIELS_WORDS) pts[(size_t)(n + 2 * m + 1) * NIELS_WORDS + t0] = bshift[t0];
+  // grid-stride over quads (the stride is a multiple of 4, so a quad stays together)
+  for (uint32_t t = t0; (t >> 2) < m; t += gridDim.x * blockDim.x) {
+    const uint32_t j = t >> 2;
+    if (kcache.table) {               // registered key: [2^128]A = comb[32][0]
+      uint32_t w[8];
+      ld_words8(vk + (size_t)key_rep[j] * 32, w);
+      const int ci = kc_lookup(kcache, w);
+      if (ci >= 0) {
+        if ((t & 3) == 0)
+          copy_record(pts, 1 + n + m + j, kcache.comb + ((size_t)ci * COMB_ENTRIES + COMB_SHIFT128) * NIELS_WORDS);
+        continue;
+      }
     }
+    const ge_niels a = ld_niels(pts, 1 + n + j);
+    ge_p3 P;
+    P.X = fe_mul(fe_sub(a.ypx, a.ymx), fe_inv2());
+    P.Y = fe_mul(fe_add(a.ypx, a.ymx), fe_inv2());
+    P.Z = fe_one();
+    P.T = fe_mul(P.X, P.Y);
+    for (int k = 0; k < 128; ++k) P = quad_dbl(P);
+    const fe zi = fe_invert(P.Z);     // every lane of the quad holds the same point
+    ge_p3 Q;
+    Q.X = fe_mul(P.X, zi);
+    Q.Y = fe_mul(P.Y, zi);
+    Q.Z = fe_one();
+    Q.T = fe_mul(Q.X, Q.Y);
+    if ((t & 3) == 0) st_niels(pts, 1 + n + m + j, ge_to_niels_affine(Q));
   }
-  const ge_niels a = ld_niels(pts, 1 + n + j);
-  ge_p3 P;
-  P.X = fe_mul(fe_sub(a.ypx, a.ymx), fe_inv2());
-  P.Y = fe_mul(fe_add(a.ypx, a.ymx), fe_inv2());
-  P.Z = fe_one();
-  P.T = fe_mul(P.X, P.Y);
-  for (int k = 0; k < 128; ++k) P = quad_dbl(P);
-  const fe zi = fe_invert(P.Z);       // every lane of the quad holds the same point
-  ge_p3 Q;
-  Q.X = fe_mul(P.X, zi);
-  Q.Y = fe_mul(P.Y, zi);
-  Q.Z = fe_one();
-  Q.T = fe_mul(Q.X, Q.Y);
-  if ((t & 3) == 0) st_niels(pts, 1 + n + m + j, ge_to_niels_affine(Q));
 }
 
 __device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t salt) {
@@ -354,13 +359,14 @@ __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned lo
                                                    const unsigned long long* __restrict__ u_acc,
                                                    uint32_t* __restrict__ scal,
                                                    const int* __restrict__ flags) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   const bool few = few_key_mode(n, m);
-  if (j < m) {
+  for (uint32_t j = j0; j < m; j += gridDim.x * blockDim.x) {
     sc a = reduce_limb_sums(key_acc + (size_t)j * PL);
     store_coeff(scal, 1 + n + j, n + m + 1 + j, a, few);
   }
+  const uint32_t j = j0;
   if (j == 0) {
     sc u = reduce_limb_sums(u_acc);
     store_coeff(scal, 0, n + 2 * m + 1, sc_sub(sc_zero(), u), few);
@@ -373,6 +379,7 @@ __global__ void k_init_basepoint(uint32_t* pts) {
 
 // ---------------------------------------------------------------- launchers
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+static inline uint32_t grid_cap(uint32_t g, uint32_t cap) { return g < cap ? g : cap; }
 
 void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                       const uint8_t* msg, const uint64_t* off, uint32_t* k) {
@@ -386,10 +393,11 @@ void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint
   if (!n) return;
   // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
   // on the device and surplus blocks exit at once
-  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
+  hipLaunchKernelGGL(k_key_points, dim3(grid_cap(cdiv(n, 256), 2048)), dim3(256), 0, st, n, vk, key_rep, pts,
+                     flags, kc);
   if (n >= FEW_KEY_MIN_N)
-    hipLaunchKernelGGL(k_key_shift, dim3(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64)), dim3(64), 0, st, n,
-                       vk, key_rep, pts, bshift, flags, kc);
+    hipLaunchKernelGGL(k_key_shift, dim3(grid_cap(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64), 1024)),
+                       dim3(64), 0, st, n, vk, key_rep, pts, bshift, flags, kc);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
@@ -408,8 +416,8 @@ void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t*
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
                        key_index, scal, key_acc, u_acc, flags);
-  hipLaunchKernelGGL(k_key_final, dim3(cdiv(n > 0 ? n : 1, 256)), dim3(256), 0, st, n, key_acc, u_acc,
-                     scal, flags);
+  hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
+                     u_acc, scal, flags);
 }
 void launch_init_basepoint(hipStream_t st, uint32_t* pts) {
   hipLaunchKernelGGL(k_init_basepoint, dim3(1), dim3(64), 0, st, pts);

@@ -1,0 +1,53 @@
+"""Kernel-timeline summary of a pipelined bench run from a rocprofv3 --kernel-trace CSV:
+GPU busy (union of kernel intervals) vs wall span, time at each concurrency level, and per-kernel
+busy share over the last `--window` k_challenge launches (the steady state).
+Usage: python tools/timeline.py <kernel_trace.csv> [--batches 20]"""
+import argparse
+import csv
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--batches", type=int, default=20)
+    a = ap.parse_args()
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name") or r.get("KernelName") or r.get("Name")
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0]))
+    rows.sort()
+    ch = [r for r in rows if "k_challenge" in r[2]]
+    if len(ch) < a.batches + 1:
+        raise SystemExit("not enough batches in trace")
+    t0 = ch[-a.batches - 1][0]
+    t1 = max(e for s, e, n in rows)
+    sel = [(max(s, t0), min(e, t1), n) for s, e, n in rows if e > t0 and s < t1]
+    ev = []
+    for s, e, n in sel:
+        ev.append((s, 1))
+        ev.append((e, -1))
+    ev.sort()
+    level = defaultdict(int)
+    cur, last = 0, t0
+    for t, d in ev:
+        level[cur] += t - last
+        cur += d
+        last = t
+    span = t1 - t0
+    busy = span - level[0]
+    per = defaultdict(int)
+    for s, e, n in sel:
+        per[n] += e - s
+    print(f"span {span/1e6:.3f} ms over {a.batches} batches = {span/1e6/a.batches:.3f} ms/batch; "
+          f"GPU busy {busy/span*100:.1f} %")
+    for k in sorted(level):
+        print(f"  concurrency {k}: {level[k]/span*100:.1f} %")
+    tot = sum(per.values())
+    for n, v in sorted(per.items(), key=lambda x: -x[1]):
+        print(f"  {n:40s} {v/1e6/a.batches:.3f} ms/batch (kernel-time {v/tot*100:.1f} %)")
+
+
+if __name__ == "__main__":
+    main()
