@@ -65,8 +65,7 @@ __global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t
                                                        uint32_t* __restrict__ pts, int* __restrict__ flags,
                                                        KeyCacheView kcache) {
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  // grid-stride: the grid is sized for the largest possible m, but capped, so a few-key batch
-  // does not dispatch thousands of waves that only read m and exit
+  // grid-stride (any grid size is correct)
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
     uint32_t w[8];
     ld_words8(vk + (size_t)key_rep[j] * 32, w);
@@ -165,7 +164,16 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
     if (cur == 0xFFFFFFFFu) {
       uint32_t prev = atomicCAS(&table[h], 0xFFFFFFFFu, i);
       if (prev == 0xFFFFFFFFu) {
-        uint32_t kidx = (uint32_t)atomicAdd(&flags[FLAG_NKEYS], 1);
+        // dense key index: one counter atomic per wave for all lanes claiming in this round
+        // (distinct-key batches claim on every lane; a per-lane atomic on one address serializes)
+        const uint64_t act = __ballot(1);
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t lane = __lane_id();
+        const uint32_t rank = (uint32_t)__popcll(act & ((1ull << lane) - 1));
+        uint32_t base = 0;
+        if ((int)lane == leader) base = (uint32_t)atomicAdd(&flags[FLAG_NKEYS], __popcll(act));
+        base = __shfl(base, leader);
+        uint32_t kidx = base + rank;
         slot_key[h] = kidx;
         key_rep[kidx] = i;
         key_slot_of_sig[i] = h;
@@ -393,8 +401,9 @@ void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint
   if (!n) return;
   // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
   // on the device and surplus blocks exit at once
-  hipLaunchKernelGGL(k_key_points, dim3(grid_cap(cdiv(n, 256), 2048)), dim3(256), 0, st, n, vk, key_rep, pts,
-                     flags, kc);
+  // one lane per possible key (a distinct-key batch decodes n keys at full occupancy, VALU-bound
+  // like k_decompress); lanes beyond the device-side m exit at once
+  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
   if (n >= FEW_KEY_MIN_N)
     hipLaunchKernelGGL(k_key_shift, dim3(grid_cap(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64), 1024)),
                        dim3(64), 0, st, n, vk, key_rep, pts, bshift, flags, kc);
