@@ -1,7 +1,7 @@
 """Kernel-timeline summary of a pipelined bench run from a rocprofv3 --kernel-trace CSV:
 GPU busy (union of kernel intervals) vs wall span, time at each concurrency level, and per-kernel
 busy share over the last `--window` k_challenge launches (the steady state).
-Usage: python tools/timeline.py <kernel_trace.csv> [--batches 20]"""
+Usage: python tools/timeline.py <kernel_trace.csv> [--batches 20] [--skip-last 1]"""
 import argparse
 import csv
 from collections import defaultdict
@@ -11,6 +11,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--skip-last", type=int, default=1,
+                    help="trailing batches to drop (bench.py's instrumented --profile-steps batches run alone)")
     a = ap.parse_args()
     rows = []
     with open(a.csv) as f:
@@ -19,10 +21,10 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0]))
     rows.sort()
     ch = [r for r in rows if "k_challenge" in r[2]]
-    if len(ch) < a.batches + 1:
+    if len(ch) < a.batches + a.skip_last + 1:
         raise SystemExit("not enough batches in trace")
-    t0 = ch[-a.batches - 1][0]
-    t1 = max(e for s, e, n in rows)
+    t0 = ch[-a.batches - a.skip_last - 1][0]
+    t1 = ch[-a.skip_last - 1][0] if a.skip_last else max(e for s, e, n in rows)
     sel = [(max(s, t0), min(e, t1), n) for s, e, n in rows if e > t0 and s < t1]
     ev = []
     for s, e, n in sel:
