@@ -258,6 +258,19 @@ def main():
                     traffic = t.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        valu = None                    # rocprof VALU counters of the same kernel (profiles/valu_pmc.json)
+        vpath = os.path.join(ROOT, "profiles", "valu_pmc.json")
+        if os.path.exists(vpath):
+            try:
+                v = json.load(open(vpath))
+                if v.get("n") == n:
+                    kd = v["kernels"]["k_decompress"]
+                    valu = {"valu_insts_per_launch": kd["valu_insts"], "mad_insts_per_launch": kd["int64_insts"],
+                            "executed_mad_frac_of_peak": round(kd["int64_lane_ops_per_cycle_per_simd"] / 16.0, 3),
+                            "valu_issue_frac": kd["valu_issue_frac"],
+                            "source": "profiles/valu_pmc.json (SQ_INSTS_VALU, SQ_INSTS_VALU_INT64, GRBM_GUI_ACTIVE)"}
+            except Exception:
+                valu = None
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
@@ -281,7 +294,7 @@ def main():
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "pmc_valu": valu,
                          "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": units,
                          "avg_launch_ms": dom_ms,
                          "measured": f"HIP events on the slot stream around each launch, {max(1, args.profile_steps)} "

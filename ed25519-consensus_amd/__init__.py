@@ -42,6 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
+    "edc_set_key_grouping",
 ]
 
 
@@ -126,6 +127,7 @@ def load_library(path=None):
         lib.edc_keycache_clear.argtypes = [c_vp]
         lib.edc_keycache_size.restype = c_sz
         lib.edc_keycache_size.argtypes = [c_vp]
+        lib.edc_set_key_grouping.argtypes = [c_vp, ctypes.c_int]
         if path is None:
             _lib = lib
         return lib
@@ -252,6 +254,10 @@ class Engine:
         with self._lock:
             u = self._check(self.lib.edc_keycache_load(self.ctx, n, b"".join(encs) or b"\0", ok))
         return u, [bool(b) for b in ok.raw[:n]]
+
+    def set_key_grouping(self, mode):
+        """0 auto (default), 1 always group keys, 2 never (one A term per signature)."""
+        self._check(self.lib.edc_set_key_grouping(self.ctx, int(mode)))
 
     def keycache_clear(self):
         with self._lock:

@@ -50,6 +50,8 @@ struct Slot {
   hipEvent_t ev[PH_N + 1] = {};
   bool pending = false;         // submitted, not yet waited
   bool timed = false;
+  bool per_sig = false;         // this batch skipped key grouping (adaptive grouping)
+  uint32_t n_batch = 0;
   int64_t ticket = -1;
 };
 
@@ -74,6 +76,10 @@ struct edc_ctx {
   float last_ms[PH_N] = {};
   int nlast = 0;
   int64_t next_ticket = 0;
+  // adaptive key grouping (edc_set_key_grouping): mode 0 = auto, 1 = always group, 2 = never
+  int key_grouping = 0;
+  double last_key_ratio = 0.0;  // distinct keys / signatures of the last grouped batch
+  int ungrouped_run = 0;        // consecutive ungrouped batches since the last grouped one
   // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
   uint32_t *kc_table = nullptr, *kc_keys = nullptr, *kc_comb = nullptr;
   uint8_t* kc_ok = nullptr;
@@ -266,21 +272,33 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
   CK(hipMemsetAsync(s.u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
   CK(hipMemsetAsync(s.d_out, 0, 256, st));
+  // Key grouping (the reference's HashMap<VerificationKeyBytes, _>, src/batch.rs:114-137) only
+  // saves work when keys repeat. When the last grouped batch had almost only distinct keys, the
+  // key terms stay per signature (A_i with coefficient z_i k_i): the same group element, so the
+  // same verdict and [8]check, without the hash table and the per-key atomics. Auto mode groups
+  // every 8th batch anyway, to notice when keys start repeating.
+  const bool per_sig = ctx->key_grouping == 2 ||
+                       (ctx->key_grouping == 0 && N >= 4096 && ctx->last_key_ratio > 0.5 && ctx->ungrouped_run < 7);
+  s.per_sig = per_sig;
+  s.n_batch = N;
   mark(PH_KEYS);
-  launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
-              s.pts, s.key_acc, s.flags);
+  if (per_sig)
+    launch_keys_per_sig(st, N, s.flags);
+  else
+    launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
+                s.pts, s.key_acc, s.flags);
   // fork: distinct keys are decoded (and, few-key mode, shifted by 2^128) on the side stream
   // while the main stream hashes and decodes the R_i; joined before the bucket accumulation
   // reads them
   CK(hipEventRecord(s.fork, st));
   CK(hipStreamWaitEvent(s.side, s.fork, 0));
-  launch_key_points(s.side, N, d_vk, s.key_rep, s.pts, ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags,
-                    ctx->kc());
+  launch_key_points(s.side, N, d_vk, per_sig ? nullptr : s.key_rep, s.pts,
+                    ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags, ctx->kc());
   CK(hipEventRecord(s.join, s.side));
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
-  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags);
+  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags, per_sig);
   mark(PH_MSM_BIN);
   launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
   // the R_i are decoded last, right before the accumulation gathers them, so the freshly written
@@ -310,6 +328,14 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
   }
   const int verdict = reinterpret_cast<int*>(s.h_out)[0];
   const int bad = reinterpret_cast<int*>(s.h_out)[1];
+  if (&s != &ctx->comb && s.n_batch) {
+    if (s.per_sig) {
+      ctx->ungrouped_run++;
+    } else {
+      ctx->ungrouped_run = 0;
+      ctx->last_key_ratio = (double)reinterpret_cast<int*>(s.h_out)[2] / (double)s.n_batch;
+    }
+  }
   if (check8) {
     if (bad) memset(check8, 0, 32);
     else memcpy(check8, s.h_out + 16, 32);
@@ -810,6 +836,13 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
   launch_chacha_fill(ctx->st(), k, blk0, nblocks, reinterpret_cast<uint32_t*>(d_out));
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->st()));
+  return 0;
+}
+
+int edc_set_key_grouping(edc_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return EDC_ERR_ARG;
+  ctx->key_grouping = mode;
+  ctx->ungrouped_run = 0;
   return 0;
 }
 

@@ -14,9 +14,11 @@ void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
                  uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
+// per-signature key terms (no grouping): m = n, key j is signature j's own key (key_rep = null)
+void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags);
+                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 // edc_msm.hip
 void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,

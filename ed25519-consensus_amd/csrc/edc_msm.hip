@@ -696,6 +696,7 @@ __global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restr
   const int bad = flags[FLAG_BAD];
   reinterpret_cast<int*>(out)[0] = (!bad && ge_is_identity(c8)) ? 0 : 1;
   reinterpret_cast<int*>(out)[1] = bad;
+  reinterpret_cast<int*>(out)[2] = flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
   if (want_compress) {
     uint32_t w8[8];
     ge_compress(c8, w8);

@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t
   // grid-stride (any grid size is correct)
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
     uint32_t w[8];
-    ld_words8(vk + (size_t)key_rep[j] * 32, w);
+    ld_words8(vk + (size_t)(key_rep ? key_rep[j] : j) * 32, w);
     const int ci = kc_lookup(kcache, w);
     if (ci >= 0) {                  // registered key: A = comb[0][0], decoded once per context
       copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(64) k_key_shift(uint32_t n, const uint8_t* __r
     const uint32_t j = t >> 2;
     if (kcache.table) {               // registered key: [2^128]A = comb[32][0]
       uint32_t w[8];
-      ld_words8(vk + (size_t)key_rep[j] * 32, w);
+      ld_words8(vk + (size_t)(key_rep ? key_rep[j] : j) * 32, w);
       const int ci = kc_lookup(kcache, w);
       if (ci >= 0) {
         if ((t & 3) == 0)
@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               uint32_t* __restrict__ scal,
                                               unsigned long long* __restrict__ key_acc,
                                               unsigned long long* __restrict__ u_acc,
-                                              int* __restrict__ flags) {
+                                              int* __restrict__ flags, int per_sig) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
@@ -294,6 +294,16 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
       uint4* sp = reinterpret_cast<uint4*>(scal + (size_t)(1 + i) * 8);
       sp[0] = make_uint4(z[0], z[1], z[2], z[3]);
       sp[1] = make_uint4(0, 0, 0, 0);
+      if (per_sig) {               // ungrouped keys: A_i's coefficient is z_i k_i mod l itself
+        uint32_t x[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) x[j] = j < PL ? v[j] : 0u;
+        const sc a = sc_reduce_wide(x);
+        uint4* ap = reinterpret_cast<uint4*>(scal + (size_t)(1 + n + i) * 8);
+        ap[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        ap[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+        continue;
+      }
       const uint32_t key = key_index[i];
       const uint32_t slot = key & (COEF_SLOTS - 1);
       const uint32_t prev = atomicCAS(&tag[slot], 0xFFFFFFFFu, key);
@@ -366,11 +376,11 @@ __device__ __forceinline__ void store_coeff(uint32_t* scal, uint32_t p, uint32_t
 __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned long long* __restrict__ key_acc,
                                                    const unsigned long long* __restrict__ u_acc,
                                                    uint32_t* __restrict__ scal,
-                                                   const int* __restrict__ flags) {
+                                                   const int* __restrict__ flags, int per_sig) {
   const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   const bool few = few_key_mode(n, m);
-  for (uint32_t j = j0; j < m; j += gridDim.x * blockDim.x) {
+  for (uint32_t j = j0; j < (per_sig ? 0u : m); j += gridDim.x * blockDim.x) {
     sc a = reduce_limb_sums(key_acc + (size_t)j * PL);
     store_coeff(scal, 1 + n + j, n + m + 1 + j, a, few);
   }
@@ -417,16 +427,19 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index);
 }
+void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags) {
+  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags + FLAG_NKEYS), (int)n, 1, st);
+}
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags) {
+                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
-                       key_index, scal, key_acc, u_acc, flags);
+                       key_index, scal, key_acc, u_acc, flags, per_sig ? 1 : 0);
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
-                     u_acc, scal, flags);
+                     u_acc, scal, flags, per_sig ? 1 : 0);
 }
 void launch_init_basepoint(hipStream_t st, uint32_t* pts) {
   hipLaunchKernelGGL(k_init_basepoint, dim3(1), dim3(64), 0, st, pts);

@@ -192,6 +192,16 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
                            uint8_t* d_out);
 
 /*
+ * Key grouping policy. The reference coalesces signatures by raw key bytes (HashMap,
+ * src/batch.rs:114-137) so each distinct key is one MSM term; this only saves work when keys
+ * repeat. mode 0 (default, auto): group, unless the last grouped batch on this context had more
+ * distinct keys than half its signatures, in which case the next batches (regrouping every 8th)
+ * keep one A_i term per signature with coefficient z_i k_i. mode 1: always group. mode 2: never.
+ * Every mode gives the same group element, hence identical verdicts and [8]*check.
+ */
+int edc_set_key_grouping(edc_ctx* ctx, int mode);
+
+/*
  * Pre-allocate the workspaces of every in-flight slot for batches of up to n items (otherwise
  * they grow on first use). Not a reference API: a setup call for streaming callers.
  */
