@@ -14,15 +14,38 @@
 
 namespace edc {
 
-#ifndef EDC_SHA_WAVES
-#define EDC_SHA_WAVES 4
-#endif
-__global__ void __launch_bounds__(256, EDC_SHA_WAVES) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
+constexpr int SHA_CLASSES = 16;   // block counts 1..14, 15+, and out-of-range lanes
+constexpr int SHA_THREADS = 256;  // items regrouped per workgroup
+__global__ void __launch_bounds__(SHA_THREADS, 4) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
                                                    const uint8_t* __restrict__ sig,
                                                    const uint8_t* __restrict__ msg,
                                                    const uint64_t* __restrict__ off,
                                                    uint32_t* __restrict__ k_out) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // Variable-length messages: a wave runs as many SHA-512 blocks as its longest message, so the
+  // workgroup's 256 items are first regrouped by block count (LDS counting sort) and each lane
+  // hashes the item at its sorted position; waves then hold messages of similar length.
+  // Equal-length batches keep the identity order.
+  __shared__ uint32_t cls_cnt[SHA_CLASSES], cls_base[SHA_CLASSES];
+  __shared__ uint32_t order[SHA_THREADS];
+  const uint32_t t = threadIdx.x;
+  const uint32_t i0 = blockIdx.x * blockDim.x + t;
+  uint32_t cls = SHA_CLASSES - 1;                     // out-of-range lanes sort last
+  if (i0 < n) {
+    const uint64_t nb = (64 + (off[i0 + 1] - off[i0]) + 17 + 127) / 128;
+    cls = nb < SHA_CLASSES - 1 ? (uint32_t)nb - 1 : SHA_CLASSES - 2;
+  }
+  if (t < SHA_CLASSES) cls_cnt[t] = 0;
+  __syncthreads();
+  const uint32_t rank = atomicAdd(&cls_cnt[cls], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int c = 0; c < SHA_CLASSES; ++c) { cls_base[c] = run; run += cls_cnt[c]; }
+  }
+  __syncthreads();
+  order[cls_base[cls] + rank] = i0;
+  __syncthreads();
+  const uint32_t i = order[t];
   if (i >= n) return;
   uint64_t o0 = off[i], o1 = off[i + 1];
   sha_src s{sig + (size_t)i * 64, vk + (size_t)i * 32, msg + o0, o1 - o0};
@@ -401,7 +424,8 @@ static inline uint32_t grid_cap(uint32_t g, uint32_t cap) { return g < cap ? g :
 
 void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                       const uint8_t* msg, const uint64_t* off, uint32_t* k) {
-  if (n) hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, sig, msg, off, k);
+  if (n)
+    hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, SHA_THREADS)), dim3(SHA_THREADS), 0, st, n, vk, sig, msg, off, k);
 }
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags) {
   if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
