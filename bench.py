@@ -116,8 +116,8 @@ CONFIGS = {   # BASELINE.json configs: (items per GPU, validators (0 = distinct 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="workload; c3 (configs[2]) is the one BASELINE.json's metric is quoted on")
     ap.add_argument("--n", type=int, default=None, help="signatures per GPU per step (default: the config's)")
