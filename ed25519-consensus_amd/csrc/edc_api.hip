@@ -305,8 +305,8 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   // point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
   launch_decompress(st, N, d_sig, s.pts, s.flags);
+  mark(PH_MSM_BUCKET);                             // (the join wait counts to the accumulation phase)
   CK(hipStreamWaitEvent(st, s.join, 0));
-  mark(PH_MSM_BUCKET);
   launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
   mark(PH_MSM_TAIL);
   launch_msm_tail(st, s.counts, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
