@@ -30,10 +30,10 @@ EDC_HD bool fe_sqrt_ratio_i(const fe& u, const fe& v, fe& r) {
   fe v7 = fe_mul(fe_sqr(v3), v);
   r = fe_mul(fe_mul(u, v3), fe_pow_p58(fe_mul(u, v7)));
   fe check = fe_mul(v, fe_sqr(r));
-  fe neg_u = fe_neg(u);
-  bool correct = fe_eq(check, u);
-  bool flipped = fe_eq(check, neg_u);
-  bool flipped_i = fe_eq(check, fe_mul(neg_u, fe_sqrtm1()));
+  // a == b (mod p) tested as canon(a - b) == 0: one canonicalisation per test instead of two
+  bool correct = fe_is_zero(fe_sub(check, u));                        // check == u
+  bool flipped = fe_is_zero(fe_add(check, u));                        // check == -u
+  bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u, fe_sqrtm1())));  // check == -u * sqrt(-1)
   fe r_prime = fe_mul(fe_sqrtm1(), r);
   r = fe_select(r, r_prime, flipped || flipped_i);
   r = fe_select(r, fe_neg(r), fe_is_negative(r));
