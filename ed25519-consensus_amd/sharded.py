@@ -45,3 +45,31 @@ def torch_allgather_fn(dist, device):
         return [host[i * len(rec):(i + 1) * len(rec)] for i in range(world)]
 
     return fn
+
+
+def find_invalid_sharded(shard_ok_fn, find_fn, allgather_obj_fn, rank, world, lo):
+    """Multi-GPU fallback after a failed global batch (the caller's verify_single loop
+    of reference tests/batch.rs:37-43). Every shard's own partial satisfies [8]P_g == 0 when all of
+    its items are valid, so only the ranks whose partial fails localize their invalid items
+    (edc_find_invalid_device on the local slice, per-item codes == Item::verify_single). The
+    (global queue index, code) pairs are all-gathered; every rank returns the same sorted list.
+
+    shard_ok_fn() -> bool      this rank's partial alone verifies ([8]P_g == 0, nothing undecodable)
+    find_fn() -> [(i, code)]   invalid items of the local slice, local indices, codes 1 / 2
+    allgather_obj_fn(obj) -> list of per-rank objects (rank order)
+    """
+    local = [] if shard_ok_fn() else [(lo + i, c) for i, c in find_fn()]
+    recs = allgather_obj_fn(local)
+    assert len(recs) == world
+    return sorted(x for r in recs for x in r)
+
+
+def torch_allgather_obj_fn(dist):
+    """all_gather_object over the default process group (small per-rank lists)."""
+    def fn(obj):
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, obj)
+        return [list(map(tuple, o)) for o in out]
+
+    return fn
+

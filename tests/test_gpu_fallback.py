@@ -77,3 +77,55 @@ def test_corpus_mixed_batch_grouped_fallback(engine, n, keys):
     code, c8 = engine.batch_verify([vks[i] for i in keep], [sigs[i] for i in keep], [msgs[i] for i in keep],
                                    z_seed=zseed, want_check8=True)
     assert code == 0 and c8 == bytes([1]) + bytes(31)
+
+
+def test_sharded_fallback_on_one_gpu(engine):
+    """sharded.find_invalid_sharded with 4 shards on one GPU: each shard's partial
+    (edc_batch_partial_device at its global z offset) alone decides whether the shard holds an
+    invalid item; only failing shards run edc_find_invalid_device on their slice; the gathered
+    global indices and codes equal Item::verify_single's."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+    from importlib import import_module
+    sharded = import_module("ed25519_consensus_amd.sharded")
+    dev = torch.device("cuda:0")
+    rnd = random.Random(2024)
+    n, keys, world = 20000, 50, 4
+    seeds = [rnd.randbytes(32) for _ in range(keys)]
+    msgs = [rnd.randbytes(rnd.randrange(0, 300)) for _ in range(n)]
+    vks, sigs = engine.sign(seeds, msgs, seed_index=[i % keys for i in range(n)])
+    expect = {}
+    for p in (123, 5001, 5002):                                   # shards 0 and 1; 2 and 3 clean
+        msgs[p] = msgs[p] + b"!"
+        expect[p] = 1
+    dec = [c for c in golden("decode.json")["cases"] if not c["ok"]]
+    vks[19999] = bytes.fromhex(dec[0]["enc"])                     # shard 3: undecodable key
+    expect[19999] = 2
+    offs = [0]
+    for m in msgs:
+        offs.append(offs[-1] + len(m))
+    d_vk, d_sig, d_msg = _dev(torch, b"".join(vks), dev), _dev(torch, b"".join(sigs), dev), _dev(torch, b"".join(msgs), dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    zseed = rnd.randbytes(32)
+    lib = engine.lib
+    found = []
+    bounds = sharded.shard_bounds(n, world)
+    for rank, (lo, hi) in enumerate(bounds):
+        m = hi - lo
+        args = (d_vk.data_ptr() + 32 * lo, d_sig.data_ptr() + 64 * lo, d_msg.data_ptr(), d_off.data_ptr() + 8 * lo)
+
+        def shard_ok():
+            part = ctypes.create_string_buffer(128)
+            bad = ctypes.c_int(0)
+            assert lib.edc_batch_partial_device(engine.ctx, m, *args, zseed, lo, None, part, ctypes.byref(bad)) == 0
+            return engine.combine_partials([part.raw], bad.value, want_check8=False)[0] == 0
+
+        def find():
+            v = ctypes.create_string_buffer(m)
+            assert lib.edc_find_invalid_device(engine.ctx, m, *args, zseed, 1024, v) >= 0
+            return [(i, c) for i, c in enumerate(v.raw) if c]
+
+        found.append(sharded.find_invalid_sharded(shard_ok, find, lambda obj: [obj], 0, 1, lo))
+    assert sorted(x for f in found for x in f) == sorted(expect.items())
+    assert found[2] == []

@@ -69,3 +69,46 @@ def test_two_rank_sharded_verify(tmp_path, name):
         res = json.load(open(out + f".{r}"))
         assert res["code"] == b["expect_code"]
         assert res["check8"] == b["expect_check8"]
+
+
+def _fallback_worker(rank, world, port, name, out_path):
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_c
+    from conftest import load_pkg
+    load_pkg()
+    from importlib import import_module
+    sharded = import_module("ed25519_consensus_amd.sharded")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == name][0]
+    items = [(bytes.fromhex(v), bytes.fromhex(s), bytes.fromhex(m)) for v, s, m in b["items"]]
+    seed = bytes.fromhex(b["z_seed"])
+    lo, hi = sharded.shard_bounds(len(items), world)[rank]
+
+    def shard_ok():
+        part, bad = oracle_c.shard_partial_affine(items[lo:hi], seed, lo)
+        code, _ = oracle_c.combine_affine([part])
+        return not bad and code == 0
+
+    def find():   # the GPU runs edc_find_invalid_device here; the oracle verifies item by item
+        return [(i, c) for i, c in enumerate(oracle_c.verify(*it) for it in items[lo:hi]) if c]
+
+    res = sharded.find_invalid_sharded(shard_ok, find, sharded.torch_allgather_obj_fn(dist), rank, world, lo)
+    with open(out_path + f".{rank}", "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["two_bad_of_300", "mixed_corpus_one_bad", "batch_verify_32"])
+def test_two_rank_sharded_fallback(tmp_path, name):
+    world = 2
+    out = str(tmp_path / "fb")
+    mp.start_processes(_fallback_worker, args=(world, _free_port(), name, out), nprocs=world, join=True,
+                       start_method="spawn")
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == name][0]
+    expect = [[i, c] for i, c in enumerate(b["expect_single"]) if c]
+    for r in range(world):
+        assert json.load(open(out + f".{r}")) == expect
+
