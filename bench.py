@@ -294,7 +294,7 @@ def main():
             except Exception:
                 valu = None
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
             cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
         line = {
             "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
