@@ -186,6 +186,7 @@ EDC_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t j) {
 #endif
     return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
   }
+  if (j >= mlen) return j == mlen ? (0x80ull << 56) : 0ull;   // padding only: marker or zeros
   uint64_t w = 0;
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
