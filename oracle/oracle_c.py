@@ -90,16 +90,24 @@ def baseline(vks, sigs, msgs, threads=None, chunk=0):
     return secs, bool(ok.value), threads
 
 
-def baseline_c3(n_sample=8192, keys=150, msg_len=120, data=None):
-    """Bounded sample of the bench workload shape (C3: repeated validator keys)."""
+def baseline_c3(n_sample=8192, keys=150, msg_len=120, data=None, min_seconds=1.5, max_reps=16):
+    """Bounded sample of the bench workload shape (C3: repeated validator keys). The sample is
+    verified repeatedly until min_seconds of wall time (~20-30 CPU-seconds on 16 threads) have
+    been timed; the rate is all verified signatures over all timed seconds."""
     if data is None:
         raise ValueError("pass data=(vks, sigs, msgs) sampled from the GPU-generated workload")
     vks, sigs, msgs = data
     threads = host_threads()
-    secs, ok, threads = baseline(vks, sigs, msgs, threads=threads)
-    return {"value": round(len(vks) / secs, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
-            "ok": ok, "seconds": round(secs, 3),
+    total, reps, ok = 0.0, 0, True
+    while reps < max_reps and (reps == 0 or total < min_seconds):
+        secs, ok_r, threads = baseline(vks, sigs, msgs, threads=threads)
+        total += secs
+        reps += 1
+        ok = ok and ok_r
+    return {"value": round(reps * len(vks) / total, 1), "unit": "sigs/s", "cores": threads, "kind": "port",
+            "ok": ok, "seconds": round(total, 3), "repeats": reps,
             "sample": f"{len(vks)} sigs of the same workload ("
                       f"{f'{keys} validators' if keys else 'distinct keys'}, "
                       f"{f'{msg_len}-byte' if msg_len >= 0 else '0..1024-byte'} msgs), "
-                      f"one Verifier per thread over {threads} equal chunks, queue+verify timed"}
+                      f"one Verifier per thread over {threads} equal chunks, queue+verify timed, "
+                      f"{reps} repeats ({round(total * threads, 1)} CPU-seconds)"}
