@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_set_key_grouping",
+    "edc_set_key_grouping", "edc_batch_submit",
 ]
 
 
@@ -104,6 +104,8 @@ def load_library(path=None):
         lib.edc_batch_submit_device.restype = ctypes.c_int64
         lib.edc_batch_submit_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                 ctypes.c_int]
+        lib.edc_batch_submit.restype = ctypes.c_int64
+        lib.edc_batch_submit.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, ctypes.c_uint64, ctypes.c_int]
         lib.edc_batch_wait.argtypes = [c_vp, ctypes.c_int64, c_vp, c_vp, ctypes.POINTER(ctypes.c_int)]
         lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_verify_each_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]
@@ -172,6 +174,7 @@ class Engine:
         if not self.ctx:
             raise EngineError(f"edc_create({device}) failed")
         self._lock = threading.Lock()
+        self._host_inflight = {}        # ticket -> host buffers borrowed by edc_batch_submit
 
     def close(self):
         if self.ctx:
@@ -201,6 +204,29 @@ class Engine:
             else:
                 rc = self.lib.edc_batch_verify(self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0", arena,
                                                offs, bytes(z_seed), check8)
+        self._check(rc)
+        return rc, (check8.raw if check8 is not None else None)
+
+    def batch_submit(self, vks, sigs, msgs, z_seed, z_base=0, want_check8=False):
+        """Asynchronous host-buffer batch (edc_batch_submit): returns a ticket; the staged host
+        buffers are kept alive here until batch_wait(ticket)."""
+        n = len(vks)
+        arena, offs = _arena(msgs)
+        bufs = (b"".join(vks) or b"\0", b"".join(sigs) or b"\0", arena, offs, bytes(z_seed))
+        with self._lock:
+            t = self.lib.edc_batch_submit(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], bufs[4], z_base,
+                                          1 if want_check8 else 0)
+            if t < 0:
+                self._check(t)
+            self._host_inflight[t] = bufs
+        return t
+
+    def batch_wait(self, ticket, want_check8=False):
+        """Verdict of a submitted batch: (code, check8 or None); the ticket's host buffers are released."""
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            rc = self.lib.edc_batch_wait(self.ctx, ticket, check8, None, None)
+            self._host_inflight.pop(ticket, None)
         self._check(rc)
         return rc, (check8.raw if check8 is not None else None)
 

@@ -48,6 +48,11 @@ struct Slot {
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
   hipEvent_t ev[PH_N + 1] = {};
+  // host-buffer submissions (edc_batch_submit): this slot's own device copy of the inputs
+  uint8_t *in_vk = nullptr, *in_sig = nullptr, *in_msg = nullptr;
+  uint64_t* in_off = nullptr;
+  size_t in_cap_n = 0, in_cap_msg = 0;
+  std::vector<uint64_t> in_rebased;   // offsets rebased to 0 (host side, alive until the slot is reused)
   bool pending = false;         // submitted, not yet waited
   bool timed = false;
   bool per_sig = false;         // this batch skipped key grouping (adaptive grouping)
@@ -251,6 +256,53 @@ static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
   return 0;
 }
 
+// Stage host inputs into slot s's own device buffers on the slot's stream (edc_batch_submit), so
+// the copy of one batch overlaps the kernels of the batches already in flight on other slots.
+static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                       const uint64_t* msg_off) {
+  if (n && (!vk || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+  int rc = init_slot(ctx, s);
+  if (rc) return rc;
+  const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
+  if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
+  if (n > s.in_cap_n || !s.in_vk) {
+    CK(hipStreamSynchronize(s.st));
+    void* in[] = {s.in_vk, s.in_sig, s.in_off};
+    for (void* p : in)
+      if (p) (void)hipFree(p);
+    s.in_vk = s.in_sig = nullptr;
+    s.in_off = nullptr;
+    s.in_cap_n = 0;
+    const size_t cap = n < 1024 ? 1024 : n + n / 8;
+    CK(dalloc(&s.in_vk, cap * 32));
+    CK(dalloc(&s.in_sig, cap * 64));
+    CK(dalloc(&s.in_off, cap + 1));
+    s.in_cap_n = cap;
+  }
+  if (mbytes > s.in_cap_msg || !s.in_msg) {
+    CK(hipStreamSynchronize(s.st));
+    if (s.in_msg) (void)hipFree(s.in_msg);
+    s.in_msg = nullptr;
+    s.in_cap_msg = 0;
+    const size_t cap = mbytes < 4096 ? 4096 : mbytes + mbytes / 8;
+    CK(dalloc(&s.in_msg, cap));
+    s.in_cap_msg = cap;
+  }
+  if (!n) return 0;
+  hipStream_t st = s.st;
+  const uint64_t* off = msg_off;
+  if (msg_off[0] != 0) {
+    s.in_rebased.resize(n + 1);
+    for (size_t i = 0; i <= n; ++i) s.in_rebased[i] = msg_off[i] - msg_off[0];
+    off = s.in_rebased.data();
+  }
+  CK(hipMemcpyAsync(s.in_off, off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  if (mbytes) CK(hipMemcpyAsync(s.in_msg, msg + msg_off[0], mbytes, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(s.in_vk, vk, n * 32, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(s.in_sig, sig, n * 64, hipMemcpyHostToDevice, st));
+  return 0;
+}
+
 // Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
 static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                          const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
@@ -406,6 +458,11 @@ void edc_destroy(edc_ctx* ctx) {
   for (Slot& s : ctx->slot) {
     if (s.st) (void)hipStreamSynchronize(s.st);
     free_slot_buffers(s);
+    {
+      void* in[] = {s.in_vk, s.in_sig, s.in_msg, s.in_off};
+      for (void* p : in)
+        if (p) (void)hipFree(p);
+    }
     if (s.flags) (void)hipFree(s.flags);
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.h_out) (void)hipHostFree(s.h_out);
@@ -476,6 +533,22 @@ int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, con
   Slot& s = ctx->slot[ticket % kSlots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, want_check8 != 0);
+  if (rc) return rc;
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int64_t edc_batch_submit(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t z_seed[32], uint64_t z_base, int want_check8) {
+  if (!ctx || !z_seed) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % kSlots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = upload_slot(ctx, s, n, vk, sig, msg, msg_off);
+  if (rc) return rc;
+  rc = enqueue_batch(ctx, s, n, s.in_vk, s.in_sig, s.in_msg, s.in_off, z_seed, z_base, nullptr, want_check8 != 0);
   if (rc) return rc;
   s.ticket = ticket;
   ctx->next_ticket++;

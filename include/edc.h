@@ -89,6 +89,16 @@ int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, con
 int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad);
 
 /*
+ * Host-buffer form of edc_batch_submit_device (replaces src/batch.rs:149 `Verifier::verify` for a
+ * caller streaming consecutive batches from host memory): the inputs are copied into the slot's
+ * own device buffers on the slot's stream, so the PCIe transfer of this batch overlaps the kernels
+ * of the batches already in flight. Host buffers are borrowed until edc_batch_wait(ticket)
+ * returns. Waited with edc_batch_wait; same ticket rules.
+ */
+int64_t edc_batch_submit(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t z_seed[32], uint64_t z_base, int want_check8);
+
+/*
  * Multi-GPU shard: evaluate this shard's part of the batch equation WITHOUT the cofactor /
  * identity step. partial (128 bytes) = canonical X||Y||Z||T of the shard's check point;
  * *bad = 1 if any item of the shard failed decoding / canonicity. Items are the shard's slice

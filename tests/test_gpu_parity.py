@@ -252,3 +252,44 @@ def test_async_submit_wait_two_in_flight(engine, edc):
     for b, code, c8 in results:
         assert code == b["expect_code"], b["name"]
         assert c8.hex() == b["expect_check8"], b["name"]
+
+
+def test_host_submit_wait_in_flight(engine):
+    """edc_batch_submit (host buffers staged per slot, copies overlapping the batches in flight):
+    every golden batch, four at a time, gives the fixture's verdict and [8]*check."""
+    bs = golden("batches.json")["batches"]
+    pending, results = [], []
+    for b in bs + bs:                                   # two passes: every slot is reused
+        if len(pending) == 4:
+            t0, b0 = pending.pop(0)
+            results.append((b0, engine.batch_wait(t0, want_check8=True)))
+        it = _items(b)
+        t = engine.batch_submit([v for v, _, _ in it], [s for _, s, _ in it], [m for _, _, m in it],
+                                bytes.fromhex(b["z_seed"]), want_check8=True)
+        pending.append((t, b))
+    while pending:
+        t0, b0 = pending.pop(0)
+        results.append((b0, engine.batch_wait(t0, want_check8=True)))
+    assert len(results) == 2 * len(bs)
+    for b, (code, c8) in results:
+        assert code == b["expect_code"], b["name"]
+        assert c8 == (bytes.fromhex(b["expect_check8"]) if b["expect_check8"] is not None else bytes(32)), b["name"]
+
+
+def test_host_submit_offsets_not_zero_based(engine):
+    """msg_off[0] != 0 (a caller's arena slice): offsets are rebased on the host, same verdict."""
+    import ctypes
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == "repeated_keys_varlen"][0]
+    it = _items(b)
+    prefix = b"\xAA" * 7
+    arena = prefix + b"".join(m for _, _, m in it)
+    offs = (ctypes.c_uint64 * (len(it) + 1))()
+    offs[0] = len(prefix)
+    for i, (_, _, m) in enumerate(it):
+        offs[i + 1] = offs[i] + len(m)
+    c8 = ctypes.create_string_buffer(32)
+    vks, sigs = b"".join(v for v, _, _ in it), b"".join(s for _, s, _ in it)
+    t = engine.lib.edc_batch_submit(engine.ctx, len(it), vks, sigs, arena, offs, bytes.fromhex(b["z_seed"]), 0, 1)
+    assert t >= 0
+    assert engine.lib.edc_batch_wait(engine.ctx, t, c8, None, None) == b["expect_code"]
+    assert c8.raw.hex() == b["expect_check8"]

@@ -1,0 +1,89 @@
+"""Host-resident (PCIe-inclusive) batch verification rate: `edc_batch_verify` with the inputs in
+host memory, as a Rust caller would hand them over (src/batch.rs:149 `Verifier::verify`). Each
+call uploads vk / sig / message arena / offsets to the context's staging buffers and runs the
+batch synchronously. This is NOT bench.py's `value` (inputs resident in HBM); DESIGN.md quotes it
+next to the device-resident rate.
+
+  python tools/host_bench.py [--config c3] [--steps 10] [--inflight 4]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=4)
+    args = ap.parse_args()
+    n, keys, msg_len, desc = bench.CONFIGS[args.config]
+    import torch
+    dev = torch.device("cuda:0")
+    torch.zeros(1, device=dev)
+    pkg = bench.load_pkg()
+    eng = pkg.Engine(0)
+    vk, sig, msg, off = bench.make_workload(pkg, eng, torch, dev, n, keys, msg_len, 0)
+    torch.cuda.synchronize()
+    zseed = bytes([0x33]) * 32
+    lib = eng.lib
+    out = {"config": desc, "n": n}
+    for kind in ("pageable", "pinned"):
+        pin = kind == "pinned"
+        hv, hs, hm, ho = (t.cpu().pin_memory() if pin else t.cpu() for t in (vk, sig, msg, off))
+        ptr = lambda t: ctypes.cast(ctypes.c_void_p(t.data_ptr()), ctypes.c_char_p)   # borrowed, not copied
+        optr = ctypes.cast(ctypes.c_void_p(ho.data_ptr()), ctypes.POINTER(ctypes.c_uint64))
+
+        def step():
+            rc = lib.edc_batch_verify(eng.ctx, n, ptr(hv), ptr(hs), ptr(hm), optr, zseed, None)
+            assert rc == 0, f"valid synthetic batch rejected: {rc} {eng.lib.edc_last_error(eng.ctx)}"
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        el = time.perf_counter() - t0
+        nbytes = hv.numel() + hs.numel() + hm.numel() + ho.numel() * 8
+        out[kind] = {"sigs_per_s": round(n * args.steps / el, 1), "ms_per_batch": round(el / args.steps * 1e3, 3),
+                     "h2d_bytes_per_batch": nbytes, "bytes_per_sig": round(nbytes / n, 1)}
+
+        # streaming: edc_batch_submit with 4 batches in flight, so batch i+1's PCIe copy runs
+        # under the kernels of batches i, i-1, ...
+        pending = []
+
+        def wait_oldest():
+            rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
+            assert rc == 0, f"valid synthetic batch rejected: {rc} {eng.lib.edc_last_error(eng.ctx)}"
+
+        def stream(k):
+            for _ in range(k):
+                if len(pending) >= args.inflight:
+                    wait_oldest()
+                t = lib.edc_batch_submit(eng.ctx, n, ptr(hv), ptr(hs), ptr(hm), optr, zseed, 0, 0)
+                assert t >= 0, eng.lib.edc_last_error(eng.ctx)
+                pending.append(t)
+            while pending:
+                wait_oldest()
+
+        stream(args.warmup)
+        t0 = time.perf_counter()
+        stream(args.steps)
+        el = time.perf_counter() - t0
+        out[kind + "_streamed"] = {"sigs_per_s": round(n * args.steps / el, 1),
+                                   "ms_per_batch": round(el / args.steps * 1e3, 3), "inflight": args.inflight}
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
