@@ -1,0 +1,50 @@
+"""GPU: the largest single-GPU batch of the BASELINE configs (configs[4] is 2^24 signatures over
+8 GPUs; here all 2^24 on ONE GPU, distinct keys, 32-byte messages, signed on the GPU). A valid
+batch is Ok with [8]*check = identity in both key-grouping modes (the first batch is grouped:
+2^25-slot hash table; auto mode then keeps distinct-key batches per signature); one corrupted s
+byte makes the batch fail, and the grouped fallback localizes exactly that item
+(InvalidSignature), as the caller's Item::verify_single loop (reference tests/batch.rs:37-43)
+would. Size-independent properties only: the oracle is not run at this size."""
+import ctypes
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_max_single_gpu_batch_2_24(engine):
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    n = 1 << 24
+    pkg = sys.modules["ed25519_consensus_amd"]
+    vk, sig, msg, off = bench.make_workload(pkg, engine, torch, dev, n, 0, 32, 0)
+    torch.cuda.synchronize()
+    lib = engine.lib
+    zseed = bytes([0x33]) * 32
+    c8 = ctypes.create_string_buffer(32)
+
+    def verify():
+        return lib.edc_batch_verify_device(engine.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                           off.data_ptr(), zseed, 0, None, c8)
+
+    assert verify() == 0 and c8.raw == bytes([1]) + bytes(31)      # grouped (first batch on the context)
+    assert verify() == 0 and c8.raw == bytes([1]) + bytes(31)      # auto: per-signature key terms
+    bad = 12345677
+    sig[64 * bad + 40] ^= 0x01                                     # s changed: still < l, wrong value
+    torch.cuda.synchronize()
+    assert verify() == 1 and c8.raw != bytes([1]) + bytes(31)     # decodable, non-identity [8]*check
+    verdicts = ctypes.create_string_buffer(n)
+    nbad = lib.edc_find_invalid_device(engine.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                       off.data_ptr(), zseed, 1 << 16, verdicts)
+    assert nbad == 1
+    raw = verdicts.raw
+    assert raw[bad] == 1
+    assert raw.count(0) == n - 1
+    del vk, sig, msg, off
+    torch.cuda.empty_cache()
