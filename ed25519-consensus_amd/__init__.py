@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_set_key_grouping", "edc_batch_submit",
+    "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed",
 ]
 
 
@@ -106,6 +106,9 @@ def load_library(path=None):
                                                 ctypes.c_int]
         lib.edc_batch_submit.restype = ctypes.c_int64
         lib.edc_batch_submit.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, ctypes.c_uint64, ctypes.c_int]
+        lib.edc_batch_submit_indexed.restype = ctypes.c_int64
+        lib.edc_batch_submit_indexed.argtypes = [c_vp, c_sz, ctypes.POINTER(ctypes.c_uint32), c_u8p, c_u8p, c_u64p,
+                                                 c_u8p, ctypes.c_uint64, ctypes.c_int]
         lib.edc_batch_wait.argtypes = [c_vp, ctypes.c_int64, c_vp, c_vp, ctypes.POINTER(ctypes.c_int)]
         lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_verify_each_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]
@@ -216,6 +219,20 @@ class Engine:
         with self._lock:
             t = self.lib.edc_batch_submit(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], bufs[4], z_base,
                                           1 if want_check8 else 0)
+            if t < 0:
+                self._check(t)
+            self._host_inflight[t] = bufs
+        return t
+
+    def batch_submit_indexed(self, key_idx, sigs, msgs, z_seed, z_base=0, want_check8=False):
+        """edc_batch_submit with keys given as positions in the last keycache_load list."""
+        n = len(sigs)
+        arena, offs = _arena(msgs)
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        bufs = (idx, b"".join(sigs) or b"\0", arena, offs, bytes(z_seed))
+        with self._lock:
+            t = self.lib.edc_batch_submit_indexed(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], bufs[4], z_base,
+                                                  1 if want_check8 else 0)
             if t < 0:
                 self._check(t)
             self._host_inflight[t] = bufs

@@ -51,6 +51,7 @@ struct Slot {
   // host-buffer submissions (edc_batch_submit): this slot's own device copy of the inputs
   uint8_t *in_vk = nullptr, *in_sig = nullptr, *in_msg = nullptr;
   uint64_t* in_off = nullptr;
+  uint32_t* in_idx = nullptr;         // key indices (edc_batch_submit_indexed)
   size_t in_cap_n = 0, in_cap_msg = 0;
   std::vector<uint64_t> in_rebased;   // offsets rebased to 0 (host side, alive until the slot is reused)
   bool pending = false;         // submitted, not yet waited
@@ -90,6 +91,8 @@ struct edc_ctx {
   uint8_t* kc_ok = nullptr;
   uint32_t* bcomb = nullptr;    // comb table of B, built with the first cache
   uint32_t kc_m = 0, kc_tmask = 0;
+  uint32_t* kc_reg = nullptr;   // registered position -> cache index (edc_batch_submit_indexed)
+  uint32_t kc_reg_m = 0;
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
     if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0};
@@ -259,24 +262,26 @@ static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
 // Stage host inputs into slot s's own device buffers on the slot's stream (edc_batch_submit), so
 // the copy of one batch overlaps the kernels of the batches already in flight on other slots.
 static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
-                       const uint64_t* msg_off) {
-  if (n && (!vk || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+                       const uint64_t* msg_off, const uint32_t* key_idx = nullptr) {
+  if (n && ((!vk && !key_idx) || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
   int rc = init_slot(ctx, s);
   if (rc) return rc;
   const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
   if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
   if (n > s.in_cap_n || !s.in_vk) {
     CK(hipStreamSynchronize(s.st));
-    void* in[] = {s.in_vk, s.in_sig, s.in_off};
+    void* in[] = {s.in_vk, s.in_sig, s.in_off, s.in_idx};
     for (void* p : in)
       if (p) (void)hipFree(p);
     s.in_vk = s.in_sig = nullptr;
     s.in_off = nullptr;
+    s.in_idx = nullptr;
     s.in_cap_n = 0;
     const size_t cap = n < 1024 ? 1024 : n + n / 8;
     CK(dalloc(&s.in_vk, cap * 32));
     CK(dalloc(&s.in_sig, cap * 64));
     CK(dalloc(&s.in_off, cap + 1));
+    CK(dalloc(&s.in_idx, cap));
     s.in_cap_n = cap;
   }
   if (mbytes > s.in_cap_msg || !s.in_msg) {
@@ -298,7 +303,13 @@ static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const
   }
   CK(hipMemcpyAsync(s.in_off, off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   if (mbytes) CK(hipMemcpyAsync(s.in_msg, msg + msg_off[0], mbytes, hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(s.in_vk, vk, n * 32, hipMemcpyHostToDevice, st));
+  if (key_idx) {                     // 4 bytes per item over PCIe instead of 32
+    CK(hipMemcpyAsync(s.in_idx, key_idx, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    launch_expand_keys(st, (uint32_t)n, s.in_idx, ctx->kc_reg, ctx->kc_keys, s.in_vk);
+    CK(hipGetLastError());
+  } else {
+    CK(hipMemcpyAsync(s.in_vk, vk, n * 32, hipMemcpyHostToDevice, st));
+  }
   CK(hipMemcpyAsync(s.in_sig, sig, n * 64, hipMemcpyHostToDevice, st));
   return 0;
 }
@@ -433,10 +444,11 @@ edc_ctx* edc_create(int device) {
 }
 
 static void free_keycache(edc_ctx* ctx) {
-  void* ptrs[] = {ctx->kc_table, ctx->kc_keys, ctx->kc_comb, ctx->kc_ok};
+  void* ptrs[] = {ctx->kc_table, ctx->kc_keys, ctx->kc_comb, ctx->kc_ok, ctx->kc_reg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  ctx->kc_table = ctx->kc_keys = ctx->kc_comb = nullptr;
+  ctx->kc_table = ctx->kc_keys = ctx->kc_comb = ctx->kc_reg = nullptr;
+  ctx->kc_reg_m = 0;
   ctx->kc_ok = nullptr;
   ctx->kc_m = ctx->kc_tmask = 0;
 }
@@ -459,7 +471,7 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.st) (void)hipStreamSynchronize(s.st);
     free_slot_buffers(s);
     {
-      void* in[] = {s.in_vk, s.in_sig, s.in_msg, s.in_off};
+      void* in[] = {s.in_vk, s.in_sig, s.in_msg, s.in_off, s.in_idx};
       for (void* p : in)
         if (p) (void)hipFree(p);
     }
@@ -547,6 +559,26 @@ int64_t edc_batch_submit(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_
   Slot& s = ctx->slot[ticket % kSlots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = upload_slot(ctx, s, n, vk, sig, msg, msg_off);
+  if (rc) return rc;
+  rc = enqueue_batch(ctx, s, n, s.in_vk, s.in_sig, s.in_msg, s.in_off, z_seed, z_base, nullptr, want_check8 != 0);
+  if (rc) return rc;
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int64_t edc_batch_submit_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx, const uint8_t* sig,
+                                 const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
+                                 uint64_t z_base, int want_check8) {
+  if (!ctx || !z_seed || (n && !key_idx)) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  uint32_t mx = 0;
+  for (size_t i = 0; i < n; ++i) mx = key_idx[i] > mx ? key_idx[i] : mx;
+  if (n && mx >= ctx->kc_reg_m) { ctx->err = "key index outside the registered key list"; return EDC_ERR_ARG; }
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % kSlots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = upload_slot(ctx, s, n, nullptr, sig, msg, msg_off, key_idx);
   if (rc) return rc;
   rc = enqueue_batch(ctx, s, n, s.in_vk, s.in_sig, s.in_msg, s.in_off, z_seed, z_base, nullptr, want_check8 != 0);
   if (rc) return rc;
@@ -833,8 +865,10 @@ int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok
   CK(dalloc(&ctx->kc_keys, (size_t)u * 8));
   CK(dalloc(&ctx->kc_ok, u));
   CK(dalloc(&ctx->kc_comb, (size_t)u * COMB_ENTRIES * NIELS_WORDS));
+  CK(dalloc(&ctx->kc_reg, m));
   CK(dalloc(&ext, (size_t)(u + 1) * EXT_WORDS));
   hipStream_t st = ctx->st();
+  CK(hipMemcpyAsync(ctx->kc_reg, of.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->kc_table, table.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->kc_keys, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   launch_kc_decode(st, u, ctx->kc_keys, ext, ctx->kc_ok);
@@ -852,6 +886,7 @@ int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok
   (void)hipFree(ext);
   ctx->kc_m = u;
   ctx->kc_tmask = T - 1;
+  ctx->kc_reg_m = (uint32_t)m;
   if (ok)
     for (size_t i = 0; i < m; ++i) ok[i] = uok[of[i]];
   return u;

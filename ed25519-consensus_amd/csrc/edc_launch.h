@@ -20,6 +20,9 @@ void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t*
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
+// vk_out[i] = keys[reg[key_idx[i]]] (32 bytes each; key-indexed host submissions)
+void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, const uint32_t* reg,
+                        const uint32_t* keys, uint8_t* vk_out);
 // edc_msm.hip
 void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);

@@ -465,6 +465,24 @@ void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t*
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
                      u_acc, scal, flags, per_sig ? 1 : 0);
 }
+// Key-indexed host submissions (edc_batch_submit_indexed): item i's raw key bytes from the key
+// cache, vk_out[i] = keys[reg[key_idx[i]]] (indices were range-checked on the host), so the
+// batch pipeline downstream sees the same 32-byte keys a per-item submission would carry.
+__global__ void __launch_bounds__(256) k_expand_keys(uint32_t n, const uint32_t* __restrict__ key_idx,
+                                                     const uint32_t* __restrict__ reg,
+                                                     const uint32_t* __restrict__ keys, uint32_t* __restrict__ vk_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* src = reinterpret_cast<const uint4*>(keys + (size_t)reg[key_idx[i]] * 8);
+  uint4* dst = reinterpret_cast<uint4*>(vk_out + (size_t)i * 8);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, const uint32_t* reg,
+                        const uint32_t* keys, uint8_t* vk_out) {
+  if (n) hipLaunchKernelGGL(k_expand_keys, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_idx, reg, keys,
+                            reinterpret_cast<uint32_t*>(vk_out));
+}
 void launch_init_basepoint(hipStream_t st, uint32_t* pts) {
   hipLaunchKernelGGL(k_init_basepoint, dim3(1), dim3(64), 0, st, pts);
 }

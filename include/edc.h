@@ -99,6 +99,16 @@ int64_t edc_batch_submit(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_
                          const uint64_t* msg_off, const uint8_t z_seed[32], uint64_t z_base, int want_check8);
 
 /*
+ * edc_batch_submit for a node whose votes come from its registered validator set: item i's key
+ * is key_idx[i], a position in the list last given to edc_keycache_load (4 bytes over PCIe per
+ * item instead of 32). The device expands the indices to the raw 32-byte keys, so verdicts and
+ * [8]*check equal edc_batch_submit with those keys. An index outside the list -> EDC_ERR_ARG.
+ */
+int64_t edc_batch_submit_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx, const uint8_t* sig,
+                                 const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
+                                 uint64_t z_base, int want_check8);
+
+/*
  * Multi-GPU shard: evaluate this shard's part of the batch equation WITHOUT the cofactor /
  * identity step. partial (128 bytes) = canonical X||Y||Z||T of the shard's check point;
  * *bad = 1 if any item of the shard failed decoding / canonicity. Items are the shard's slice

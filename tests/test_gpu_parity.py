@@ -293,3 +293,34 @@ def test_host_submit_offsets_not_zero_based(engine):
     assert t >= 0
     assert engine.lib.edc_batch_wait(engine.ctx, t, c8, None, None) == b["expect_code"]
     assert c8.raw.hex() == b["expect_check8"]
+
+
+@pytest.mark.parametrize("name", ["repeated_keys_varlen", "undecodable_A", "zip215_corpus_batch", "two_bad_of_300",
+                                  "mixed_corpus_one_bad", "c1_1024_distinct"])
+def test_host_submit_indexed_equals_fixture(engine, name):
+    """edc_batch_submit_indexed: keys as positions in the registered list (registered in reverse
+    first-occurrence order with a duplicate, so list position != cache index); same verdict and
+    [8]*check as the fixture; an index past the list is an argument error."""
+    from conftest import load_pkg
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == name][0]
+    it = _items(b)
+    distinct = list(dict.fromkeys(v for v, _, _ in it))[::-1]
+    reg = [distinct[0]] + distinct                       # position 0 duplicates position 1
+    pos = {}
+    for i, k in enumerate(reg):
+        pos.setdefault(k, i)
+    engine.keycache_load(reg)
+    try:
+        idx = [pos[v] for v, _, _ in it]
+        if idx:
+            idx[0] = 1 if idx[0] == 0 else idx[0]            # either position of the duplicated key
+        t = engine.batch_submit_indexed(idx, [s for _, s, _ in it], [m for _, _, m in it],
+                                        bytes.fromhex(b["z_seed"]), want_check8=True)
+        code, c8 = engine.batch_wait(t, want_check8=True)
+        assert code == b["expect_code"]
+        assert c8 == (bytes.fromhex(b["expect_check8"]) if b["expect_check8"] is not None else bytes(32))
+        with pytest.raises(load_pkg().EngineError):
+            engine.batch_submit_indexed([len(reg)] + idx[1:], [s for _, s, _ in it], [m for _, _, m in it],
+                                        bytes.fromhex(b["z_seed"]))
+    finally:
+        engine.keycache_clear()
