@@ -344,13 +344,6 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
                        (ctx->key_grouping == 0 && N >= 4096 && ctx->last_key_ratio > 0.5 && ctx->ungrouped_run < 7);
   s.per_sig = per_sig;
   s.n_batch = N;
-  // launch-size hint for the per-key kernels (grid-stride, so correctness never depends on it):
-  // twice the distinct keys the last grouped batch had at this batch's size, or 0 = unknown
-  uint32_t m_hint = 0;
-  if (!per_sig && ctx->last_key_ratio > 0.0) {
-    const double h = 2.0 * ctx->last_key_ratio * N + 256.0;
-    m_hint = h >= (double)N ? 0u : (uint32_t)h;
-  }
   mark(PH_KEYS);
   if (per_sig)
     launch_keys_per_sig(st, N, s.flags);
@@ -363,13 +356,12 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   CK(hipEventRecord(s.fork, st));
   CK(hipStreamWaitEvent(s.side, s.fork, 0));
   launch_key_points(s.side, N, d_vk, per_sig ? nullptr : s.key_rep, s.pts,
-                    ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags, ctx->kc(), m_hint);
+                    ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags, ctx->kc());
   CK(hipEventRecord(s.join, s.side));
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
-  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags, per_sig,
-              m_hint);
+  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags, per_sig);
   mark(PH_MSM_BIN);
   launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
   // the R_i are decoded last, right before the accumulation gathers them, so the freshly written

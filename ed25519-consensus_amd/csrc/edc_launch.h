@@ -10,7 +10,7 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
 void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags, const KeyCacheView& kc, uint32_t m_hint = 0);
+                       const uint32_t* bshift, int* flags, const KeyCacheView& kc);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
                  uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
@@ -18,8 +18,7 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
 void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig,
-                 uint32_t m_hint = 0);
+                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 // vk_out[i] = keys[reg[key_idx[i]]] (32 bytes each; key-indexed host submissions)
 void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, const uint32_t* reg,

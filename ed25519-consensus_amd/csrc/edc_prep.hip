@@ -431,20 +431,16 @@ void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t*
   if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
 }
 void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags, const KeyCacheView& kc, uint32_t m_hint) {
+                       const uint32_t* bshift, int* flags, const KeyCacheView& kc) {
   if (!n) return;
-  // m (distinct keys) is only known on the device. Both kernels are grid-stride, so any grid is
-  // correct; the grid covers the largest possible m (one lane per possible key: a distinct-key
-  // batch decodes n keys at full occupancy, VALU-bound like k_decompress) unless the host has a
-  // hint from the context's last grouped batch (m_hint > 0: twice that batch's key ratio), which
-  // spares a few-key batch thousands of exit-only workgroups.
-  const uint64_t cover = m_hint ? (m_hint < n ? m_hint : n) : n;
-  hipLaunchKernelGGL(k_key_points, dim3(cdiv(cover, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
-  if (n >= FEW_KEY_MIN_N) {
-    const uint64_t few = m_hint ? (cover < n / FEW_KEY_RATIO ? cover : n / FEW_KEY_RATIO) : n / FEW_KEY_RATIO;
-    hipLaunchKernelGGL(k_key_shift, dim3(grid_cap(cdiv(4ull * few + NIELS_WORDS, 64), 1024)),
+  // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
+  // on the device and surplus blocks exit at once
+  // one lane per possible key (a distinct-key batch decodes n keys at full occupancy, VALU-bound
+  // like k_decompress); lanes beyond the device-side m exit at once
+  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
+  if (n >= FEW_KEY_MIN_N)
+    hipLaunchKernelGGL(k_key_shift, dim3(grid_cap(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64), 1024)),
                        dim3(64), 0, st, n, vk, key_rep, pts, bshift, flags, kc);
-  }
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
@@ -460,15 +456,13 @@ void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags) {
 }
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig,
-                 uint32_t m_hint) {
+                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
                        key_index, scal, key_acc, u_acc, flags, per_sig ? 1 : 0);
-  const uint64_t cover = m_hint ? (m_hint < n ? m_hint : n) : n;   // grid-stride: any grid is correct
-  hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(cover > 0 ? cover : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
+  hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
                      u_acc, scal, flags, per_sig ? 1 : 0);
 }
 // Key-indexed host submissions (edc_batch_submit_indexed): item i's raw key bytes from the key
