@@ -48,3 +48,42 @@ def test_max_single_gpu_batch_2_24(engine):
     assert raw.count(0) == n - 1
     del vk, sig, msg, off
     torch.cuda.empty_cache()
+
+
+def test_key_indexed_stream_equals_device_path_2_20(engine):
+    """configs[2] scale (2^20 votes, 150 validators): edc_batch_submit_indexed (validator indices,
+    keys expanded on the device) gives the same verdict and [8]*check as edc_batch_verify_device
+    on the same items, for a valid batch and for one with a corrupted signature."""
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    n, keys = 1 << 20, 150
+    pkg = sys.modules["ed25519_consensus_amd"]
+    vk, sig, msg, off = bench.make_workload(pkg, engine, torch, dev, n, keys, 120, 0)
+    torch.cuda.synchronize()
+    lib = engine.lib
+    kb = bytes(vk[:32 * keys].cpu().tolist())
+    engine.keycache_load([kb[32 * i:32 * i + 32] for i in range(keys)])
+    try:
+        idx = (ctypes.c_uint32 * n)(*[i % keys for i in range(n)])
+        for corrupt in (False, True):
+            if corrupt:
+                sig[64 * 777777 + 45] ^= 0x10
+                torch.cuda.synchronize()
+            zseed = bytes([0x5A]) * 32
+            c8_dev = ctypes.create_string_buffer(32)
+            code_dev = lib.edc_batch_verify_device(engine.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                                   off.data_ptr(), zseed, 0, None, c8_dev)
+            hs, hm, ho = sig.cpu(), msg.cpu(), off.cpu()
+            ptr = lambda t: ctypes.cast(ctypes.c_void_p(t.data_ptr()), ctypes.c_char_p)
+            optr = ctypes.cast(ctypes.c_void_p(ho.data_ptr()), ctypes.POINTER(ctypes.c_uint64))
+            t = lib.edc_batch_submit_indexed(engine.ctx, n, idx, ptr(hs), ptr(hm), optr, zseed, 0, 1)
+            assert t >= 0
+            c8 = ctypes.create_string_buffer(32)
+            code = lib.edc_batch_wait(engine.ctx, t, c8, None, None)
+            assert code == code_dev == (1 if corrupt else 0)
+            assert c8.raw == c8_dev.raw
+            assert (c8.raw == bytes([1]) + bytes(31)) != corrupt
+    finally:
+        engine.keycache_clear()
