@@ -87,6 +87,38 @@ def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
     return vk, sig, msg, off
 
 
+def make_c4_workload(pkg, eng, torch, dev, n, keys, msg_len, cases, corpus_msg, pos_seed=bytes([0x44]) * 32):
+    """BASELINE configs[3]: the configs[2]-style vote batch (make_workload) with the ZIP215 small-order
+    corpus (reference tests/small_order.rs:12-77; `cases` = tests/golden/zip215_small_order.json) put
+    at seeded positions (their message is `corpus_msg`, b"Zcash") and ONE bad signature: the item at
+    another seeded position keeps its signature but its message is changed, i.e. it was signed over a
+    different message (tests/batch.rs:27-31). Positions come from random.Random(pos_seed) (SURVEY
+    8(d) seed [0x44;32]). Returns vk, sig, msg, off (device) and {index: expected verify_single code}
+    for every item whose code is not Ok, plus the corpus positions."""
+    import random
+    vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, keys, msg_len, 0)
+    rnd = random.Random(pos_seed)
+    pos = rnd.sample(range(n), len(cases) + 1)
+    cpos, bad = pos[:-1], pos[-1]
+    pt = torch.tensor(cpos, dtype=torch.int64, device=dev)
+    vk.view(-1, 32)[:n][pt] = torch.tensor([list(bytes.fromhex(c["vk"])) for c in cases], dtype=torch.uint8,
+                                           device=dev)
+    sig.view(-1, 64)[:n][pt] = torch.tensor([list(bytes.fromhex(c["sig"])) for c in cases], dtype=torch.uint8,
+                                            device=dev)
+    m2d = msg.view(n, msg_len)
+    m2d[pt, :len(corpus_msg)] = torch.tensor(list(corpus_msg), dtype=torch.uint8, device=dev)
+    m2d[bad, 0] ^= 1                               # the bad item: signed over another message
+    lens = torch.full((n,), msg_len, dtype=torch.int64, device=dev)
+    lens[pt] = len(corpus_msg)
+    cols = torch.arange(msg_len, device=dev)[None, :]
+    arena = torch.cat([m2d[cols < lens[:, None]], torch.zeros(1, dtype=torch.uint8, device=dev)])
+    off2 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    off2[1:] = torch.cumsum(lens, 0)
+    expect = {p: c["expect_single"] for p, c in zip(cpos, cases) if c["expect_single"]}
+    expect[bad] = 1
+    return vk, sig, arena, off2, expect, cpos
+
+
 def cpu_baseline(vk, sig, msg, off, n_sample, keys, msg_len):
     """Oracle C restatement (dalek u64-backend algorithm, oracle/edc_oracle.c) on the host
     cores: the first n_sample items of the SAME GPU-generated workload, one Verifier per

@@ -1,15 +1,17 @@
 """BASELINE configs[3] timing: a 2^20-vote batch (150 validators, 120-byte messages) with the 196
-ZIP215 corpus cases and one bad signature mixed in. Times, device-resident:
+ZIP215 small-order corpus cases (tests/golden/zip215_small_order.json, message "Zcash") and one
+signature made over another message mixed in at seeded positions (bench.make_c4_workload). Times,
+device-resident:
   batch      the failing batch verification (edc_batch_verify_device)
   per_sig    the reference's fallback, Item::verify_single on every item (edc_verify_each_device)
-  grouped    the bisection fallback (edc_find_invalid_device)
-and checks that both fallbacks flag exactly the bad item.
-  python tools/fallback_bench.py [--n 1048576] [--leaf 16384]"""
+  grouped    the grouped fallback (edc_find_invalid_device)
+and checks that both fallbacks return exactly the expected per-item codes (the bad item
+InvalidSignature, every corpus case and every other vote Ok). Prints one JSON line.
+  python tools/fallback_bench.py [--n 1048576] [--leaf 65536] [--keycache]"""
 import argparse
 import ctypes
 import json
 import os
-import random
 import sys
 import time
 
@@ -23,7 +25,8 @@ def main():
     ap.add_argument("--keys", type=int, default=150)
     ap.add_argument("--msg-len", type=int, default=120)
     ap.add_argument("--leaf", type=int, default=65536)
-    ap.add_argument("--leaf-cached", type=int, default=0, help="grouped-fallback leaf with the key cache")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--keycache", action="store_true", help="also time with the validator keys in the key cache")
     args = ap.parse_args()
     import torch
     import bench
@@ -33,64 +36,57 @@ def main():
     eng = pkg.Engine(0)
     lib = eng.lib
     n = args.n
-    vk, sig, msg, off = bench.make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, 0)
-    torch.cuda.synchronize()
-    # corpus cases (fixed 69-byte messages do not fit the uniform arena; they replace whole items
-    # whose message is reused: the corpus signatures are over "Zcash", so use the golden per-item
-    # check instead -- here: one bad item, the corpus goes through tests/test_gpu_fallback.py)
-    rnd = random.Random(5)
-    bad = rnd.randrange(n)
-    m = msg.view(n, args.msg_len)
-    m[bad, 0] ^= 1
+    with open(os.path.join(ROOT, "tests", "golden", "zip215_small_order.json")) as f:
+        fx = json.load(f)
+    vk, sig, msg, off, expect, cpos = bench.make_c4_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len,
+                                                             fx["cases"], bytes.fromhex(fx["msg"]))
     torch.cuda.synchronize()
     zseed = bytes([0x33]) * 32
 
     def timed(fn):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        r = fn()
-        torch.cuda.synchronize()
-        return r, (time.perf_counter() - t0) * 1e3
+        best, r = None, None
+        for _ in range(args.reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) * 1e3
+            best = dt if best is None else min(best, dt)
+        return r, best
 
-    args_dev = (vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr())
-    lib.edc_reserve(eng.ctx, n)
-    rc, t_batch = timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
-    rc, t_batch = timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
-    assert rc == 1
+    a = (vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr())
+    eng._check(lib.edc_reserve(eng.ctx, n))
     ver = torch.zeros(n, dtype=torch.uint8, device=dev)
-    timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
-    _, t_each = timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
-    flagged_each = torch.nonzero(ver).flatten().tolist()
     verdicts = ctypes.create_string_buffer(n)
-    timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, args.leaf, verdicts))
-    nbad, t_group = timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, args.leaf, verdicts))
-    flagged_group = [i for i, c in enumerate(verdicts.raw) if c]
-    assert flagged_each == flagged_group == [bad], (flagged_each[:5], flagged_group[:5], bad)
-    out = {"n": n, "validators": args.keys, "bad_index": bad, "batch_ms": round(t_batch, 3),
-           "per_sig_fallback_ms": round(t_each, 3), "grouped_fallback_ms": round(t_group, 3),
-           "leaf": args.leaf, "per_sig_sigs_per_s": round(n / t_each * 1e3, 1)}
-    if args.keys:
-        # the same three with the validator keys registered in the context's key cache
-        keys = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
+
+    def run_all():
+        rc, t_batch = timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *a, zseed, 0, None, None))
+        assert rc == 1, rc
+        rc, t_each = timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *a, ver.data_ptr()))
+        eng._check(rc)
+        h = ver.cpu()
+        flagged_each = {int(i): int(h[i]) for i in torch.nonzero(h).flatten().tolist()}
+        nbad, t_group = timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *a, zseed, args.leaf, verdicts))
+        eng._check(nbad)
+        raw = verdicts.raw
+        flagged_group = {i: raw[i] for i in range(n) if raw[i]}
+        assert flagged_each == flagged_group == expect, (flagged_each, flagged_group, expect)
+        return {"batch_ms": round(t_batch, 3), "per_sig_fallback_ms": round(t_each, 3),
+                "grouped_fallback_ms": round(t_group, 3), "grouped_over_batch": round(t_group / t_batch, 3),
+                "per_sig_sigs_per_s": round(n / t_each * 1e3, 1)}
+
+    out = {"workload": "configs[3]: 2^20 votes / 150 validators / 120-B msgs + 196 ZIP215 corpus cases + 1 bad sig",
+           "n": n, "validators": args.keys, "corpus_cases": len(cpos), "expected_invalid": expect,
+           "leaf": args.leaf, "timing": "best of %d, device-resident, synchronous" % args.reps}
+    out.update(run_all())
+    if args.keycache and args.keys:
+        keys = bytes(vk[:32 * args.keys].cpu().tolist())
         t0 = time.perf_counter()
-        u, ok = eng.keycache_load([keys[32 * i:32 * i + 32] for i in range(len(keys) // 32)])
-        t_load = (time.perf_counter() - t0) * 1e3
-        assert all(ok)
-        timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
-        rc, t_batch_c = timed(lambda: lib.edc_batch_verify_device(eng.ctx, n, *args_dev, zseed, 0, None, None))
-        assert rc == 1
-        ver.zero_()
-        timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
-        _, t_each_c = timed(lambda: lib.edc_verify_each_device(eng.ctx, n, *args_dev, ver.data_ptr()))
-        assert torch.nonzero(ver).flatten().tolist() == [bad]
-        leaf_c = args.leaf_cached or args.leaf
-        timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, leaf_c, verdicts))
-        nbad, t_group_c = timed(lambda: lib.edc_find_invalid_device(eng.ctx, n, *args_dev, zseed, leaf_c, verdicts))
-        assert [i for i, c in enumerate(verdicts.raw) if c] == [bad]
-        out["keycache"] = {"keys": u, "load_ms": round(t_load, 3), "batch_ms": round(t_batch_c, 3),
-                           "per_sig_fallback_ms": round(t_each_c, 3), "grouped_fallback_ms": round(t_group_c, 3),
-                           "leaf": leaf_c, "per_sig_sigs_per_s": round(n / t_each_c * 1e3, 1)}
-    print(json.dumps(out))
+        u, ok = eng.keycache_load([keys[32 * i:32 * i + 32] for i in range(args.keys)])
+        out["keycache"] = {"keys": u, "load_ms": round((time.perf_counter() - t0) * 1e3, 3)}
+        out["keycache"].update(run_all())
+        eng.keycache_clear()
+    print(json.dumps(out), flush=True)
     eng.close()
 
 
