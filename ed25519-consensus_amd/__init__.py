@@ -82,8 +82,8 @@ def load_library(path=None):
     with _lib_lock:
         if _lib is not None and path is None:
             return _lib
-        # EDC_LIB_PATH: measurement hook to load an A/B variant build of the same sources
-        p = path or os.environ.get("EDC_LIB_PATH") or LIB_PATH
+        # an explicit path is a measurement hook for tools/ (A/B builds); the product loads LIB_PATH
+        p = path or LIB_PATH
         if not os.path.exists(p):
             raise EngineError(f"HIP extension not built: {p} (run __graft_entry__.build())")
         _share_torch_hip_runtime()
@@ -165,8 +165,8 @@ def _arena(msgs):
 class Engine:
     """One C-ABI context = one GPU = one HIP stream (include/edc.h)."""
 
-    def __init__(self, device=None):
-        self.lib = load_library()
+    def __init__(self, device=None, lib_path=None):
+        self.lib = load_library(lib_path)
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         cnt = self.lib.edc_device_count()

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for v in "$@"; do
   lib=ed25519-consensus_amd/csrc/libedc_$v.so
   [ "$v" = "base" ] && lib=ed25519-consensus_amd/csrc/libedc.so
-  EDC_LIB_PATH=$PWD/$lib timeout -k 10 120 python -u bench.py --steps ${AB_STEPS:-20} --warmup 2 --no-cpu-baseline --profile-steps 3 ${AB_ARGS} > gpurun_out/ab_$v.log 2>&1
+  timeout -k 10 120 python -u bench.py --lib $PWD/$lib --steps ${AB_STEPS:-20} --warmup 2 --no-cpu-baseline --profile-steps 3 ${AB_ARGS} > gpurun_out/ab_$v.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$v FAILED rc=$rc"; tail -5 gpurun_out/ab_$v.log; [ $rc -ge 124 ] && exit $rc; continue; fi
   python3 -c "
