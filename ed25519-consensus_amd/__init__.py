@@ -42,7 +42,8 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed",
+    "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
+    "edc_set_window_bits",
 ]
 
 
@@ -113,6 +114,9 @@ def load_library(path=None):
         lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_verify_each_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]
         lib.edc_find_invalid_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_sz, c_vp]
+        lib.edc_batch_verify_fallback_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_vp,
+                                                         ctypes.POINTER(ctypes.c_int), c_vp]
+        lib.edc_set_window_bits.argtypes = [c_vp, ctypes.c_int]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]
@@ -299,8 +303,13 @@ class Engine:
         return u, [bool(b) for b in ok.raw[:n]]
 
     def set_key_grouping(self, mode):
-        """0 auto (default), 1 always group keys, 2 never (one A term per signature)."""
+        """0 auto (default), 1 always group keys, 2 never (one A term per signature), 3 test mode:
+        grouping abandoned on the device (the adversarial-key overflow path)."""
         self._check(self.lib.edc_set_key_grouping(self.ctx, int(mode)))
+
+    def set_window_bits(self, bits):
+        """Pippenger window width (0 = chosen from the batch size; 8..16 forced)."""
+        self._check(self.lib.edc_set_window_bits(self.ctx, int(bits)))
 
     def keycache_clear(self):
         with self._lock:

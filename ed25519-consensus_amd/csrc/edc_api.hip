@@ -2,8 +2,10 @@
 // Every entry point cites the reference API it replaces in include/edc.h.
 #include <string.h>
 #include <string>
+#include <random>
 #include <unordered_map>
 #include <vector>
+#include <hip/hip_ext.h>
 #include "edc.h"
 #include "edc_common.h"
 #include "edc_launch.h"
@@ -31,19 +33,21 @@ constexpr int kSlots = 4;  // batches that can be in flight per context
 // One in-flight batch: its own HIP stream and every per-batch device buffer.
 struct Slot {
   hipStream_t st = nullptr;
-  hipStream_t side = nullptr;   // key decoding (+ few-key shifts), concurrent with R decoding
-  hipEvent_t fork = nullptr, join = nullptr;
   size_t cap_n = 0, cap_T = 0;
   uint32_t *k = nullptr, *key_slot = nullptr, *key_index = nullptr, *key_rep = nullptr;
   uint32_t *table = nullptr, *slot_key = nullptr;
   uint32_t *pts = nullptr, *scal = nullptr;
   unsigned long long *key_acc = nullptr, *u_acc = nullptr;
+  uint8_t *itembad = nullptr, *keybad = nullptr;   // per-item / per-key failure bits (fallback)
+  // MSM workspace, grown on demand to the plan's bins / entries
+  uint32_t cap_bins = 0, cap_ranges = 0;
+  size_t cap_entries = 0;
   uint32_t *counts = nullptr, *offsets = nullptr, *cursor = nullptr;
   uint2* entries = nullptr;
   uint32_t* sorted = nullptr;   // entries' point indices sorted by bucket within each bin
   uint32_t *slice_W = nullptr, *slice_T = nullptr, *win = nullptr;
-  uint32_t* buckets = nullptr;  // NBIN x 256 bucket sums (extended), fixed size
-  uint32_t* heads = nullptr;    // NBIN x 256 head partials of the segmented accumulation
+  uint32_t* buckets = nullptr;  // bins x 256 bucket sums (extended)
+  uint32_t* heads = nullptr;    // bins x 256 head partials of the segmented accumulation
   int* flags = nullptr;
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
@@ -64,7 +68,7 @@ struct Slot {
 struct edc_ctx {
   int device = 0;
   std::string err;
-  uint32_t* btab = nullptr;     // [1..8]B and [2^128]B, affine Niels
+  uint32_t* btab = nullptr;     // [1..8]B, affine Niels
   Slot slot[kSlots];
   // staging for the host-pointer entry points (used on slot 0's stream)
   size_t cap_n = 0, cap_msg = 0, cap_aux = 0;
@@ -84,8 +88,18 @@ struct edc_ctx {
   int64_t next_ticket = 0;
   // adaptive key grouping (edc_set_key_grouping): mode 0 = auto, 1 = always group, 2 = never
   int key_grouping = 0;
+  bool have_key_ratio = false;  // a grouped batch has completed on this context
   double last_key_ratio = 0.0;  // distinct keys / signatures of the last grouped batch
   int ungrouped_run = 0;        // consecutive ungrouped batches since the last grouped one
+  int win_bits = 0;             // MSM window width override (edc_set_window_bits), 0 = by batch size
+  uint64_t secret = 0;          // key-grouping hash secret (OS randomness, per context)
+  uint64_t nbatches = 0;
+  // grouped fallback (range MSM) staging, slot 0 only
+  size_t fb_cap_terms = 0, fb_cap_ranges = 0;
+  uint32_t *fb_xpt = nullptr, *fb_xrg = nullptr, *fb_xscal = nullptr;
+  uint8_t* fb_rv = nullptr;      // per-range verdict | pre-bad flag
+  uint32_t* fb_idx = nullptr;    // items verified one by one
+  size_t fb_cap_idx = 0;
   // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
   uint32_t *kc_table = nullptr, *kc_keys = nullptr, *kc_comb = nullptr;
   uint8_t* kc_ok = nullptr;
@@ -109,17 +123,25 @@ struct edc_ctx {
     }                                                                   \
   } while (0)
 
+static void free_msm_buffers(Slot& s) {
+  void* ptrs[] = {s.counts, s.offsets, s.cursor, s.slice_W, s.slice_T, s.win, s.buckets, s.heads, s.entries, s.sorted};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  s.counts = s.offsets = s.cursor = s.slice_W = s.slice_T = s.win = s.buckets = s.heads = s.sorted = nullptr;
+  s.entries = nullptr;
+  s.cap_bins = s.cap_ranges = 0;
+  s.cap_entries = 0;
+}
+
 static void free_slot_buffers(Slot& s) {
   void* ptrs[] = {s.k, s.key_slot, s.key_index, s.key_rep, s.table, s.slot_key, s.pts, s.scal, s.key_acc,
-                  s.u_acc, s.counts, s.offsets, s.cursor, s.entries, s.sorted, s.slice_W, s.slice_T, s.win, s.buckets, s.heads};
+                  s.u_acc, s.itembad, s.keybad};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s.k = s.key_slot = s.key_index = s.key_rep = s.table = s.slot_key = s.pts = s.scal = nullptr;
   s.key_acc = s.u_acc = nullptr;
-  s.counts = s.offsets = s.cursor = nullptr;
-  s.entries = nullptr;
-  s.sorted = nullptr;
-  s.slice_W = s.slice_T = s.win = s.buckets = s.heads = nullptr;
+  s.itembad = s.keybad = nullptr;
+  free_msm_buffers(s);
   s.cap_n = s.cap_T = 0;
 }
 
@@ -129,12 +151,22 @@ static size_t next_pow2(size_t x) {
   return p;
 }
 
+// Every in-flight slot needs its own hardware queue: kernels of streams that share a queue run
+// in order, so one batch's latency-bound tail would stall the bulk kernels of another. Streams
+// created with an (all-CU) mask get a dedicated queue instead of one of the runtime's shared pool
+// (GPU_MAX_HW_QUEUES, 4 by default, one of which the process's default stream already holds).
+static hipError_t create_slot_stream(int device, hipStream_t* st) {
+  int cus = 0;
+  hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess || cus <= 0) return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+  std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
+  if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+  return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+}
+
 static int init_slot(edc_ctx* ctx, Slot& s) {
   if (s.st) return 0;
-  CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
-  CK(hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking));
-  CK(hipEventCreateWithFlags(&s.fork, hipEventDisableTiming));
-  CK(hipEventCreateWithFlags(&s.join, hipEventDisableTiming));
+  CK(create_slot_stream(ctx->device, &s.st));
   CK(dalloc(&s.flags, FLAG_COUNT));
   CK(dalloc(&s.d_out, 256));
   CK(hipHostMalloc((void**)&s.h_out, 256));
@@ -159,22 +191,103 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.pts, (2 + 2 * cap) * NIELS_WORDS));   // >= msm_num_points(n, m) for any m <= n
   CK(dalloc(&s.scal, (2 + 2 * cap) * 8));
   CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
-  CK(dalloc(&s.u_acc, KEY_ACC_LIMBS));
-  CK(dalloc(&s.counts, NBIN));
-  CK(dalloc(&s.offsets, NBIN));
-  CK(dalloc(&s.cursor, NBIN));
-  CK(dalloc(&s.entries, msm_entry_capacity((uint32_t)cap)));
-  CK(dalloc(&s.sorted, msm_entry_capacity((uint32_t)cap)));
-  CK(dalloc(&s.slice_W, (size_t)NBIN * EXT_WORDS));
-  CK(dalloc(&s.slice_T, (size_t)NBIN * EXT_WORDS));
-  CK(dalloc(&s.win, (size_t)NWIN_FULL * EXT_WORDS));
-  CK(dalloc(&s.buckets, msm_bucket_words()));
-  CK(dalloc(&s.heads, msm_bucket_words()));
+  CK(dalloc(&s.u_acc, (cap / COEF_CHUNK + 2) * KEY_ACC_LIMBS));   // one sum per fallback range
+  CK(dalloc(&s.itembad, cap));
+  CK(dalloc(&s.keybad, cap));
   launch_init_basepoint(s.st, s.pts);
   CK(hipGetLastError());
   s.cap_n = cap;
   s.cap_T = T;
   return 0;
+}
+
+// MSM workspace for plan P with up to `entries` digits (grow-only; the slot is idle when called)
+static int ensure_msm(edc_ctx* ctx, Slot& s, const MsmPlan& P, size_t entries) {
+  const uint32_t nbin = P.nbin();
+  if (nbin > MSM_MAX_BINS || P.nwin > MSM_MAX_WIN) { ctx->err = "MSM plan too large"; return EDC_ERR_ARG; }
+  if (nbin > s.cap_bins || P.nranges > s.cap_ranges) {
+    CK(hipStreamSynchronize(s.st));
+    for (void* p : {(void*)s.counts, (void*)s.offsets, (void*)s.cursor, (void*)s.slice_W, (void*)s.slice_T,
+                    (void*)s.win, (void*)s.buckets, (void*)s.heads})
+      if (p) (void)hipFree(p);
+    const uint32_t nb = nbin > s.cap_bins ? nbin : s.cap_bins;
+    const uint32_t nr = P.nranges > s.cap_ranges ? P.nranges : (s.cap_ranges ? s.cap_ranges : 1);
+    s.counts = s.offsets = s.cursor = s.slice_W = s.slice_T = s.win = s.buckets = s.heads = nullptr;
+    s.cap_bins = s.cap_ranges = 0;
+    CK(dalloc(&s.counts, nb));
+    CK(dalloc(&s.offsets, nb));
+    CK(dalloc(&s.cursor, nb));
+    CK(dalloc(&s.slice_W, (size_t)nb * EXT_WORDS));
+    CK(dalloc(&s.slice_T, (size_t)nb * EXT_WORDS));
+    CK(dalloc(&s.win, (size_t)nr * MSM_MAX_WIN * EXT_WORDS));
+    CK(dalloc(&s.buckets, msm_bucket_words(nb)));
+    CK(dalloc(&s.heads, msm_bucket_words(nb)));
+    s.cap_bins = nb;
+    s.cap_ranges = nr;
+  }
+  if (entries > s.cap_entries) {
+    CK(hipStreamSynchronize(s.st));
+    if (s.entries) (void)hipFree(s.entries);
+    if (s.sorted) (void)hipFree(s.sorted);
+    s.entries = nullptr;
+    s.sorted = nullptr;
+    s.cap_entries = 0;
+    const size_t cap = entries + entries / 8 + 1024;
+    CK(dalloc(&s.entries, cap));
+    CK(dalloc(&s.sorted, cap));
+    s.cap_entries = cap;
+  }
+  return 0;
+}
+
+// ---- MSM plans ----
+// Window width by batch size: wide windows amortize the 2 x buckets reduction work over many
+// points; narrow ones keep enough digits per bucket for small batches.
+static int auto_window_bits(size_t n) {
+  if (n >= (1u << 19)) return 16;
+  if (n >= (1u << 17)) return 14;
+  if (n >= (1u << 15)) return 13;
+  if (n >= (1u << 13)) return 12;
+  return 10;
+}
+
+// short windows of c bits over the 128-bit z, then windows of hi bits up to 254 (the top window
+// absorbs the last carry of a 253-bit scalar)
+static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
+  MsmPlan P{};
+  uint32_t w = 0, off = 0, bin = 0;
+  const uint32_t ws = (128 + c - 1) / c;
+  for (; w < ws; ++w, off += c) {
+    P.off[w] = (uint16_t)off;
+    P.bits[w] = (uint8_t)c;
+    uint32_t buckets = 1u << (c - 1);
+    if (w + 1 == ws && (uint32_t)c * ws == 128) buckets = 1u << c;   // unsigned top digit of a z
+    P.nslice[w] = (uint16_t)((buckets + NSLICE - 1) / NSLICE);
+    P.bin0[w] = (uint16_t)bin;
+    bin += P.nslice[w];
+  }
+  P.nwin_short = ws;
+  for (; off < 254; ++w, off += hi) {
+    P.off[w] = (uint16_t)off;
+    P.bits[w] = (uint8_t)hi;
+    P.nslice[w] = (uint16_t)(((1u << (hi - 1)) + NSLICE - 1) / NSLICE);
+    P.bin0[w] = (uint16_t)bin;
+    bin += P.nslice[w];
+  }
+  P.nwin = w;
+  P.nranges = nranges;
+  P.bins_per_range = bin;
+  return P;
+}
+
+// Batch plan: few distinct keys (consensus votes; known from the previous grouped batch on this
+// context) put the 253-bit B / key coefficients' high bits in 8-bit windows with ~m entries each
+// (one bin per window instead of 128 nearly empty ones); otherwise every window has c bits.
+// Any plan is an exact MSM: the hint only affects speed.
+static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
+  const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
+  const bool few = !per_sig && ctx->have_key_ratio && ctx->last_key_ratio * 16.0 <= 1.0 && n >= 4096;
+  return make_plan(c, few ? 8 : c, 1);
 }
 
 // host-staging buffers (inputs of the host-pointer entry points, per-item outputs)
@@ -314,10 +427,28 @@ static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const
   return 0;
 }
 
-// Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
-static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
-                         const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
-                         const uint8_t* d_z, int want_compress) {
+static uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Key grouping (the reference's HashMap<VerificationKeyBytes, _>, src/batch.rs:114-137) only
+// saves work when keys repeat. When the last grouped batch had almost only distinct keys, the
+// key terms stay per signature (A_i with coefficient z_i k_i): the same group element, so the
+// same verdict and [8]check, without the hash table and the per-key atomics. Auto mode groups
+// every 8th batch anyway, to notice when keys start repeating.
+static bool choose_per_sig(const edc_ctx* ctx, size_t n) {
+  return ctx->key_grouping == 2 || (ctx->key_grouping == 0 && n >= 4096 && ctx->have_key_ratio &&
+                                    ctx->last_key_ratio > 0.5 && ctx->ungrouped_run < 7);
+}
+
+// Enqueue the per-signature prefix of the pipeline on slot s: key grouping, SHA-512 challenges,
+// z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization.
+static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                          const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
+                          const uint8_t* d_z, bool with_bin, const MsmPlan* P, bool force_per_sig = false) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
@@ -332,48 +463,57 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
     if (s.timed) (void)hipEventRecord(s.ev[ph], st);
   };
   CK(hipMemsetAsync(s.flags, 0, FLAG_COUNT * sizeof(int), st));
-  CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
   CK(hipMemsetAsync(s.u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
   CK(hipMemsetAsync(s.d_out, 0, 256, st));
-  // Key grouping (the reference's HashMap<VerificationKeyBytes, _>, src/batch.rs:114-137) only
-  // saves work when keys repeat. When the last grouped batch had almost only distinct keys, the
-  // key terms stay per signature (A_i with coefficient z_i k_i): the same group element, so the
-  // same verdict and [8]check, without the hash table and the per-key atomics. Auto mode groups
-  // every 8th batch anyway, to notice when keys start repeating.
-  const bool per_sig = ctx->key_grouping == 2 ||
-                       (ctx->key_grouping == 0 && N >= 4096 && ctx->last_key_ratio > 0.5 && ctx->ungrouped_run < 7);
+  const bool per_sig = force_per_sig || choose_per_sig(ctx, n);
   s.per_sig = per_sig;
   s.n_batch = N;
   mark(PH_KEYS);
-  if (per_sig)
+  if (per_sig) {
     launch_keys_per_sig(st, N, s.flags);
-  else
-    launch_keys(st, N, d_vk, s.table, T - 1, seed[0] ^ 0x5bd1e995u, s.slot_key, s.key_slot, s.key_rep, s.key_index,
-                s.pts, s.key_acc, s.flags);
-  // fork: distinct keys are decoded (and, few-key mode, shifted by 2^128) on the side stream
-  // while the main stream hashes and decodes the R_i; joined before the bucket accumulation
-  // reads them
-  CK(hipEventRecord(s.fork, st));
-  CK(hipStreamWaitEvent(s.side, s.fork, 0));
-  launch_key_points(s.side, N, d_vk, per_sig ? nullptr : s.key_rep, s.pts,
-                    ctx->btab + (size_t)BTAB_BSHIFT * NIELS_WORDS, s.flags, ctx->kc());
-  CK(hipEventRecord(s.join, s.side));
+  } else {
+    CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
+    const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
+    const uint32_t salt[2] = {(uint32_t)h, (uint32_t)(h >> 32)};
+    launch_keys(st, N, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
+                s.key_index, s.key_acc, s.flags);
+  }
   mark(PH_CHALLENGE);
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
-  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.flags, per_sig);
+  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
+              per_sig);
   mark(PH_MSM_BIN);
-  launch_msm_bin(st, N, s.scal, s.counts, s.offsets, s.cursor, s.entries, s.flags);
-  // the R_i are decoded last, right before the accumulation gathers them, so the freshly written
-  // point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
+  if (with_bin) {
+    const MsmTerms terms{N, 0, 0, 0, s.scal, nullptr, nullptr, nullptr};
+    launch_msm_bin(st, *P, terms, 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  }
+  // the points are decoded last, right before the accumulation gathers them, so the freshly
+  // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
-  launch_decompress(st, N, d_sig, s.pts, s.flags);
-  mark(PH_MSM_BUCKET);                             // (the join wait counts to the accumulation phase)
-  CK(hipStreamWaitEvent(st, s.join, 0));
-  launch_msm_bucket(st, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
-  mark(PH_MSM_TAIL);
-  launch_msm_tail(st, s.counts, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
-  mark(PH_N);
+  launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc());
+  CK(hipGetLastError());
+  return 0;
+}
+
+// Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
+static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                         const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
+                         const uint8_t* d_z, int want_compress) {
+  if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
+  int rc = ensure_slot(ctx, s, n);
+  if (rc) return rc;
+  const MsmPlan P = batch_plan(ctx, n, choose_per_sig(ctx, n));
+  rc = ensure_msm(ctx, s, P, msm_entry_capacity(P, n, n + 1));
+  if (rc) return rc;
+  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P);
+  if (rc) return rc;
+  hipStream_t st = s.st;
+  if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
+  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
+  if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
+  launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
+  if (s.timed) (void)hipEventRecord(s.ev[PH_N], st);
   CK(hipGetLastError());
   CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, st));
   s.pending = true;
@@ -396,6 +536,7 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
       ctx->ungrouped_run++;
     } else {
       ctx->ungrouped_run = 0;
+      ctx->have_key_ratio = true;
       ctx->last_key_ratio = (double)reinterpret_cast<int*>(s.h_out)[2] / (double)s.n_batch;
     }
   }
@@ -430,6 +571,10 @@ int edc_device_count(void) {
 edc_ctx* edc_create(int device) {
   edc_ctx* ctx = new edc_ctx();
   ctx->device = device;
+  {
+    std::random_device rd;   // OS randomness: the key-grouping hash secret of this context
+    ctx->secret = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
+  }
   bool ok = hipSetDevice(device) == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
             dalloc(&ctx->btab, BTAB_ENTRIES * NIELS_WORDS) == hipSuccess;
   if (ok) {
@@ -454,10 +599,8 @@ static void free_keycache(edc_ctx* ctx) {
 }
 
 static int sync_all(edc_ctx* ctx) {
-  for (Slot& s : ctx->slot) {
+  for (Slot& s : ctx->slot)
     if (s.st) CK(hipStreamSynchronize(s.st));
-    if (s.side) CK(hipStreamSynchronize(s.side));
-  }
   return 0;
 }
 
@@ -480,10 +623,6 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
-    if (s.side) (void)hipStreamSynchronize(s.side);
-    if (s.fork) (void)hipEventDestroy(s.fork);
-    if (s.join) (void)hipEventDestroy(s.join);
-    if (s.side) (void)hipStreamDestroy(s.side);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   {
@@ -494,13 +633,10 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
-    if (s.fork) (void)hipEventDestroy(s.fork);
-    if (s.join) (void)hipEventDestroy(s.join);
-    if (s.side) (void)hipStreamDestroy(s.side);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
-                  ctx->btab, ctx->comb_in};
+                  ctx->btab, ctx->comb_in, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal, ctx->fb_rv, ctx->fb_idx};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete ctx;
@@ -699,92 +835,164 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
   return 0;
 }
 
-// ---- grouped fallback (bisection on partial check points) ----
-// sum of g canonical partial points (128-byte records) -> canonical sum, and the verdict of
-// [8]*sum == 0 (with the OR of the bad flags)
-static int sum_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int bad, uint8_t sum[128]) {
-  return combine_points(ctx, g, partials, bad, nullptr, sum);
+// ---- grouped fallback: one MSM pass over ~256 contiguous ranges ----
+static int ensure_fb(edc_ctx* ctx, size_t terms, size_t ranges) {
+  if (terms > ctx->fb_cap_terms || !ctx->fb_xpt) {
+    CK(hipStreamSynchronize(ctx->st()));
+    for (void* p : {(void*)ctx->fb_xpt, (void*)ctx->fb_xrg, (void*)ctx->fb_xscal})
+      if (p) (void)hipFree(p);
+    ctx->fb_xpt = ctx->fb_xrg = ctx->fb_xscal = nullptr;
+    ctx->fb_cap_terms = 0;
+    const size_t cap = terms + terms / 8 + 64;
+    CK(dalloc(&ctx->fb_xpt, cap));
+    CK(dalloc(&ctx->fb_xrg, cap));
+    CK(dalloc(&ctx->fb_xscal, cap * 8));
+    ctx->fb_cap_terms = cap;
+  }
+  if (ranges > ctx->fb_cap_ranges || !ctx->fb_rv) {
+    CK(hipStreamSynchronize(ctx->st()));
+    if (ctx->fb_rv) (void)hipFree(ctx->fb_rv);
+    ctx->fb_rv = nullptr;
+    CK(dalloc(&ctx->fb_rv, 2 * ranges + 64));
+    ctx->fb_cap_ranges = ranges;
+  }
+  return 0;
 }
 
-// canonical -P from canonical P (x -> p - x on X and T)
-static void neg_partial(const uint8_t P[128], uint8_t out[128]) {
-  static const uint8_t pbytes[32] = {0xed, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
-                                     0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
-                                     0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0x7f};
-  memcpy(out, P, 128);
-  for (int c : {0, 3}) {
-    const uint8_t* x = P + 32 * c;
-    bool zero = true;
-    for (int i = 0; i < 32; ++i) zero &= x[i] == 0;
-    if (zero) continue;
-    int borrow = 0;
-    for (int i = 0; i < 32; ++i) {
-      int d = (int)pbytes[i] - x[i] - borrow;
-      borrow = d < 0;
-      out[32 * c + i] = (uint8_t)(d + (borrow ? 256 : 0));
-    }
+// Item::verify_single (src/batch.rs:104-107) for the listed items, with the batch's queue-time k
+// (slot s): gathered into the staging buffers, one per-item launch, codes scattered into verdicts.
+static int verify_listed(edc_ctx* ctx, Slot& s, const std::vector<uint32_t>& idx, const uint8_t* d_vk,
+                         const uint8_t* d_sig, uint8_t* verdicts, int* invalid) {
+  const size_t c = idx.size();
+  if (!c) return 0;
+  int rc = ensure_n(ctx, c);
+  if (rc) return rc;
+  if (c > ctx->fb_cap_idx || !ctx->fb_idx) {
+    if (ctx->fb_idx) (void)hipFree(ctx->fb_idx);
+    ctx->fb_idx = nullptr;
+    CK(dalloc(&ctx->fb_idx, c + c / 8 + 64));
+    ctx->fb_cap_idx = c + c / 8 + 64;
   }
+  hipStream_t st = s.st;
+  CK(hipMemcpyAsync(ctx->fb_idx, idx.data(), c * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  launch_gather_items(st, (uint32_t)c, ctx->fb_idx, d_vk, d_sig, s.k, ctx->vk, ctx->sig, ctx->kbuf);
+  launch_verify_single(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts, ctx->kc(),
+                       ctx->bcomb);
+  CK(hipGetLastError());
+  std::vector<uint8_t> v(c);
+  CK(hipMemcpyAsync(v.data(), ctx->verdicts, c, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  for (size_t j = 0; j < c; ++j) {
+    verdicts[idx[j]] = v[j];
+    *invalid += v[j] != 0;
+  }
+  return 0;
+}
+
+// After a failed batch on slot s (its k, decoded points, key grouping and per-item failure bits
+// still in place): the batch equation restricted to ~256 contiguous ranges in ONE MSM pass
+// (range-tagged bins, 9-bit windows), [8]P_g == 0 per range; ranges whose check fails or that
+// hold an item with an undecodable R / key or a non-canonical s are verified item by item.
+// Items of passing ranges are valid (ZIP215: batch == single, with a fresh secret z: see
+// include/edc.h). verdicts (host, n bytes) receive Item::verify_single's code for every item.
+static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                           const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
+                           bool per_sig, uint32_t m, uint8_t* verdicts) {
+  memset(verdicts, 0, n);
+  if (!n) return 0;
+  const size_t target = (n + 255) / 256;
+  const size_t rsize = (target + COEF_CHUNK - 1) / COEF_CHUNK * COEF_CHUNK;
+  const uint32_t G = (uint32_t)((n + rsize - 1) / rsize);
+  if (!per_sig && (size_t)G * m > s.cap_n) {
+    // too many distinct keys for per-(range, key) sums: redo the prefix with one key term per
+    // signature (the same group element)
+    int rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, nullptr, false, nullptr, true);
+    if (rc) return rc;
+    CK(hipStreamSynchronize(s.st));
+    per_sig = true;
+  }
+  const MsmPlan P = make_plan(9, 9, G);
+  const uint32_t mm = per_sig ? 0u : m;
+  const size_t nx = (size_t)G * (mm + 1);
+  const uint32_t npoint = (uint32_t)(per_sig ? 2 * n : n);
+  int rc = ensure_msm(ctx, s, P, msm_entry_capacity(P, n, (per_sig ? n : 0) + nx));
+  if (rc) return rc;
+  rc = ensure_fb(ctx, nx, G);
+  if (rc) return rc;
+  uint32_t seed[8];
+  seed_words(z_seed, seed);
+  hipStream_t st = s.st;
+  launch_range_coef(st, (uint32_t)n, (uint32_t)rsize, G, m, per_sig, d_sig, s.k, nullptr, seed, z_base, s.key_index,
+                    s.scal, s.key_acc, s.u_acc, s.flags, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal);
+  const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, s.scal, ctx->fb_xpt, ctx->fb_xrg,
+                       ctx->fb_xscal};
+  launch_msm_bin(st, P, terms, npoint + (uint32_t)nx, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
+  launch_msm_range_tail(st, P, s.slice_W, s.slice_T, s.win, ctx->fb_rv);
+  CK(hipMemsetAsync(ctx->fb_rv + G, 0, G, st));
+  launch_range_prebad(st, (uint32_t)n, (uint32_t)rsize, s.itembad, s.keybad, s.key_index, per_sig, ctx->fb_rv + G);
+  CK(hipGetLastError());
+  std::vector<uint8_t> rv(2 * (size_t)G);
+  CK(hipMemcpyAsync(rv.data(), ctx->fb_rv, 2 * (size_t)G, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  std::vector<uint32_t> idx;
+  for (uint32_t g = 0; g < G; ++g)
+    if (rv[g] || rv[G + g])
+      for (size_t i = (size_t)g * rsize; i < n && i < (size_t)(g + 1) * rsize; ++i) idx.push_back((uint32_t)i);
+  int invalid = 0;
+  rc = verify_listed(ctx, s, idx, d_vk, d_sig, verdicts, &invalid);
+  if (rc) return rc;
+  return invalid;
+}
+
+// grouping state of the batch last enqueued on slot s (after it completed)
+static int slot_grouping(edc_ctx* ctx, Slot& s, bool* per_sig, uint32_t* m) {
+  int f[FLAG_COUNT];
+  CK(hipMemcpy(f, s.flags, sizeof(f), hipMemcpyDeviceToHost));
+  *per_sig = s.per_sig || f[FLAG_OVF] != 0;
+  *m = (uint32_t)f[FLAG_NKEYS];
+  return 0;
 }
 
 int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                             const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
                             size_t leaf, uint8_t* verdicts) {
+  (void)leaf;
   if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_msg_off || !verdicts))) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  if (ctx->slot[0].pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
-  if (leaf < 64) leaf = 64;
-  memset(verdicts, 0, n);
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
   if (!n) return 0;
-  struct Node { size_t lo, hi; int bad; uint8_t P[128]; };
-  auto partial = [&](size_t lo, size_t hi, Node& nd) -> int {
-    nd.lo = lo; nd.hi = hi;
-    return run_batch_sync(ctx, hi - lo, d_vk + 32 * lo, d_sig + 64 * lo, d_msg, d_msg_off + lo, z_seed, lo, nullptr,
-                          nullptr, nd.P, &nd.bad);
-  };
-  std::vector<Node> todo(1);
-  int rc = partial(0, n, todo[0]);
-  if (rc < 0) return rc;
-  if (rc == 0) { todo.clear(); }
-  int invalid = 0;
-  while (!todo.empty()) {
-    Node nd = todo.back();
-    todo.pop_back();
-    const size_t m = nd.hi - nd.lo;
-    if (m <= leaf) {   // per-item Item::verify_single on the leaf
-      rc = ensure_n(ctx, m);
-      if (rc) return rc;
-      hipStream_t st = ctx->st();
-      launch_challenge(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, d_msg, d_msg_off + nd.lo, ctx->kbuf);
-      launch_verify_single(st, (uint32_t)m, d_vk + 32 * nd.lo, d_sig + 64 * nd.lo, ctx->kbuf, ctx->btab, ctx->vtab,
-                           ctx->verdicts,
-                       ctx->kc(), ctx->bcomb);
-      CK(hipGetLastError());
-      CK(hipMemcpyAsync(verdicts + nd.lo, ctx->verdicts, m, hipMemcpyDeviceToHost, st));
-      CK(hipStreamSynchronize(st));
-      for (size_t i = 0; i < m; ++i) invalid += verdicts[nd.lo + i] != 0;
-      continue;
-    }
-    const size_t mid = nd.lo + m / 2;
-    Node L, R;
-    rc = partial(nd.lo, mid, L);
-    if (rc < 0) return rc;
-    const int bad_l = rc;
-    int bad_r;
-    if (nd.bad) {      // a decode / canonicity failure makes the parent's point meaningless
-      bad_r = partial(mid, nd.hi, R);
-      if (bad_r < 0) return bad_r;
-    } else {           // linearity: P_R = P - P_L, no item of either half failed decoding
-      uint8_t pair[256];
-      memcpy(pair, nd.P, 128);
-      neg_partial(L.P, pair + 128);
-      R.lo = mid; R.hi = nd.hi; R.bad = 0;
-      bad_r = sum_partials(ctx, 2, pair, 0, R.P);
-      if (bad_r < 0) return bad_r;
-    }
-    if (bad_r) todo.push_back(R);
-    if (bad_l) todo.push_back(L);
+  int rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, nullptr, false, nullptr);
+  if (rc) return rc;
+  CK(hipStreamSynchronize(s.st));
+  bool per_sig;
+  uint32_t m;
+  rc = slot_grouping(ctx, s, &per_sig, &m);
+  if (rc) return rc;
+  return fallback_ranges(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, per_sig, m, verdicts);
+}
+
+int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                     const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                                     uint8_t* verdicts, int* n_invalid, uint8_t check8[32]) {
+  if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_msg_off || !verdicts))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  if (n_invalid) *n_invalid = 0;
+  int rc = run_batch_sync(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, nullptr, check8, nullptr, nullptr);
+  if (rc <= 0) {
+    if (rc == 0 && n) memset(verdicts, 0, n);
+    return rc;
   }
-  return invalid;
+  Slot& s = ctx->slot[0];
+  bool per_sig;
+  uint32_t m;
+  int r2 = slot_grouping(ctx, s, &per_sig, &m);
+  if (r2) return r2;
+  r2 = fallback_ranges(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, per_sig, m, verdicts);
+  if (r2 < 0) return r2;
+  if (n_invalid) *n_invalid = r2;
+  return EDC_INVALID_SIGNATURE;
 }
 
 int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok) {
@@ -948,18 +1156,29 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
 }
 
 int edc_set_key_grouping(edc_ctx* ctx, int mode) {
-  if (!ctx || mode < 0 || mode > 2) return EDC_ERR_ARG;
+  if (!ctx || mode < 0 || mode > 3) return EDC_ERR_ARG;
   ctx->key_grouping = mode;
   ctx->ungrouped_run = 0;
+  return 0;
+}
+
+int edc_set_window_bits(edc_ctx* ctx, int bits) {
+  if (!ctx || bits < 0 || (bits && (bits < 8 || bits > 16))) return EDC_ERR_ARG;
+  ctx->win_bits = bits;
   return 0;
 }
 
 int edc_reserve(edc_ctx* ctx, size_t n) {
   if (!ctx) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
+  const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
+  const MsmPlan dense = make_plan(c, c, 1), few = make_plan(c, 8, 1);
+  const size_t e1 = msm_entry_capacity(dense, n, n + 1), e2 = msm_entry_capacity(few, n, n + 1);
   for (Slot& s : ctx->slot) {
     if (s.pending) { ctx->err = "reserve with a batch in flight"; return EDC_ERR_ARG; }
     int rc = ensure_slot(ctx, s, n);
+    if (rc) return rc;
+    rc = ensure_msm(ctx, s, dense.nbin() >= few.nbin() ? dense : few, e1 > e2 ? e1 : e2);
     if (rc) return rc;
   }
   return 0;

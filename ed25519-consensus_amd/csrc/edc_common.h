@@ -68,20 +68,51 @@ __device__ __forceinline__ void ld_words8(const uint8_t* p, uint32_t w[8]) {
   w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
 }
 
-// ---- scalar windows (Pippenger) ----
-constexpr int WIN_BITS = 16;
-constexpr int NWIN_FULL = 16;      // 253-bit coefficients (B, A keys)
-constexpr int NWIN_Z = 8;          // 128-bit z (R points), top window unsigned
+// ---- Pippenger plan: windows of the scalar bits, buckets, bins ----
+// An MSM term is (point, scalar, range). Terms with a "short" scalar (the 128-bit z_i of R_i) use
+// windows [0, nwin_short) only; full-width scalars (253-bit coefficients of B and the keys) use
+// every window. Window w covers scalar bits [off[w], off[w] + bits[w]) as a signed digit
+// (carry into the next window); the top short window is unsigned for short scalars (they have no
+// window above it), so its digit can reach 2^bits when bits divides 128. Digit magnitude m >= 1
+// goes to bucket m - 1; a bin is one slice of 256 consecutive buckets of one window of one range
+// and is reduced by one workgroup. Ranges (>1 only in the grouped fallback) are independent MSMs
+// over contiguous slices of the signatures.
+constexpr int MSM_MAX_WIN = 32;
 constexpr int SLICE_BITS = 8;      // 256 buckets per slice (one workgroup)
-constexpr int NSLICE = 256;        // slices per window (window 7 needs buckets up to 2^16)
-constexpr int NBIN = NWIN_FULL * NSLICE;
+constexpr int NSLICE = 1 << SLICE_BITS;
+constexpr uint32_t MSM_MAX_BINS = 8192;
 
-// signed radix-2^16 recoding. For z scalars (nwin = 8) the last digit is left unsigned and
-// may reach 2^16 (no carry out of bit 128); for 253-bit scalars no carry leaves window 15.
-__device__ __forceinline__ int scalar_digit(const uint32_t s[8], int w, int& carry, bool top_unsigned) {
-  uint32_t raw = ((s[w >> 1] >> ((w & 1) * 16)) & 0xFFFFu) + (uint32_t)carry;
+struct MsmPlan {
+  uint32_t nwin, nwin_short;
+  uint32_t nranges;
+  uint32_t bins_per_range;        // sum of nslice over the windows
+  uint16_t off[MSM_MAX_WIN];      // first scalar bit of window w
+  uint8_t bits[MSM_MAX_WIN];      // width of window w (<= 16)
+  uint16_t bin0[MSM_MAX_WIN];     // first bin of window w inside a range
+  uint16_t nslice[MSM_MAX_WIN];   // slices of window w
+  __host__ __device__ uint32_t nbin() const { return nranges * bins_per_range; }
+};
+
+// The terms of one MSM. Batch (rsize = 0): point terms t = 0..n+m (B, R_i, keys), range 0.
+// Ranges (grouped fallback, rsize > 0): point terms t < npoint are R_i (t < n, point 1+t, range
+// t / rsize) and, for one key term per signature, A_i (point 1+t, range (t-n) / rsize); then nx
+// listed terms (point xpt, range xrg, scalar xscal): the per-(range, key) and per-range B terms.
+struct MsmTerms {
+  uint32_t n, rsize, npoint, nx;
+  const uint32_t* scal;
+  const uint32_t* xpt;
+  const uint32_t* xrg;
+  const uint32_t* xscal;
+};
+
+// signed digit of window w (bits <= 16) with carry in/out; top_unsigned keeps the raw value
+__device__ __forceinline__ int plan_digit(const uint32_t s[8], uint32_t off, uint32_t bits, int& carry,
+                                          bool top_unsigned) {
+  const uint32_t k = off >> 5, sh = off & 31;
+  const uint64_t two = (uint64_t)s[k] | ((uint64_t)(k < 7 ? s[k + 1] : 0u) << 32);
+  const uint32_t raw = ((uint32_t)(two >> sh) & ((1u << bits) - 1u)) + (uint32_t)carry;
   if (top_unsigned) { carry = 0; return (int)raw; }
-  if (raw >= 0x8000u) { carry = 1; return (int)raw - 0x10000; }
+  if (raw >= (1u << (bits - 1))) { carry = 1; return (int)raw - (int)(1u << bits); }
   carry = 0;
   return (int)raw;
 }
@@ -89,29 +120,18 @@ __device__ __forceinline__ int scalar_digit(const uint32_t s[8], int w, int& car
 // 64-bit limb-sum accumulators per distinct key (12 limbs of a 128 x 256-bit product)
 constexpr int KEY_ACC_LIMBS = 12;
 
-// flags slot indices (FLAG_WINMASK: bit w set when MSM window w has at least one entry)
-enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_WINMASK = 3, FLAG_COUNT = 8 };
+// flags slot indices. FLAG_OVF: key grouping gave up (probe limit, section "Key grouping" of
+// DESIGN.md): the batch continues with one key term per signature, which is the same group element.
+enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_COUNT = 8 };
 
-// Few-key batches (consensus votes: m validators << n votes). Every full-width coefficient
-// (B and each distinct key) is split as c = c_lo + 2^128 c_hi over the points P and
-// [2^128]P, so EVERY scalar of the MSM is < 2^128 and only the 8 low windows exist: half the
-// bucket reductions and half the Horner doublings. The shifted key points cost 128 doublings
-// per key, computed on a side stream under the R decompression; [2^128]B is a context
-// constant. Point layout in few-key mode:
-//   0 = B, 1..n = R_i, n+1..n+m = A_j, n+m+1..n+2m = [2^128]A_j, n+2m+1 = [2^128]B.
-constexpr uint32_t FEW_KEY_MIN_N = 4096;
-constexpr int BTAB_BSHIFT = 8;     // context table entry holding [2^128]B
-constexpr int BTAB_ENTRIES = 9;
-constexpr uint32_t FEW_KEY_RATIO = 16;
-__host__ __device__ __forceinline__ bool few_key_mode(uint32_t n, uint32_t m) {
-  return n >= FEW_KEY_MIN_N && (uint64_t)m * FEW_KEY_RATIO <= n;
-}
-__host__ __device__ __forceinline__ uint32_t msm_num_points(uint32_t n, uint32_t m) {
-  return few_key_mode(n, m) ? n + 2 * m + 2 : 1 + n + m;
-}
-// point p of the MSM carries a scalar < 2^128 (8 windows, top digit unsigned)?
-__device__ __forceinline__ bool msm_short_scalar(uint32_t p, uint32_t n, bool few) {
-  return few || (p >= 1 && p <= n);
-}
+// Points of a batch MSM: 0 = B, 1..n = R_i, n+1..n+m = the distinct keys (grouped) or each
+// signature's own key (m = n, one key term per signature).
+__host__ __device__ __forceinline__ uint32_t msm_num_points(uint32_t n, uint32_t m) { return 1 + n + m; }
+
+constexpr int BTAB_ENTRIES = 8;
+constexpr uint32_t COEF_CHUNK = 2048;   // signatures per k_coef workgroup (range sizes are multiples)   // context table [1..8]B (per-item fallback, signer)
+
+// Per-item failure bits written by the prefix kernels (the grouped fallback reads them).
+enum { ITEM_BAD_S = 1, ITEM_BAD_R = 2 };
 
 }  // namespace edc

@@ -3,38 +3,51 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "keycache.h"
+#include "edc_common.h"
 
 namespace edc {
 // edc_prep.hip
 void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
-void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags);
-void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags, const KeyCacheView& kc);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
+                       bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
+                       const KeyCacheView& kc);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
-                 uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
-                 uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags);
+                 const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
+                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags);
 // per-signature key terms (no grouping): m = n, key j is signature j's own key (key_rep = null)
 void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig);
+                 unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
+                 bool per_sig);
+// grouped fallback: per-(range, key) / per-range coefficients as listed MSM terms
+void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nranges, uint32_t m, bool per_sig,
+                       const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],
+                       uint64_t zbase, const uint32_t* key_index, uint32_t* scal, unsigned long long* key_acc,
+                       unsigned long long* u_acc, int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal);
+void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* keybad,
+                         const uint32_t* key_index, bool per_sig, uint8_t* rbad);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
+void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const uint8_t* vk, const uint8_t* sig,
+                         const uint32_t* k, uint8_t* out_vk, uint8_t* out_sig, uint32_t* out_k);
 // vk_out[i] = keys[reg[key_idx[i]]] (32 bytes each; key-indexed host submissions)
 void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, const uint32_t* reg,
                         const uint32_t* keys, uint8_t* vk_out);
 // edc_msm.hip
-void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
+void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);
-void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
+void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
                        uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T);
-size_t msm_bucket_words();
-void launch_msm_tail(hipStream_t st, const uint32_t* counts, const uint32_t* slice_W, const uint32_t* slice_T,
+size_t msm_bucket_words(uint32_t nbin);
+void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out);
+void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
+                           uint32_t* win, uint8_t* rverdict);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
                     uint8_t* out);
-size_t msm_entry_capacity(uint32_t n);
+size_t msm_entry_capacity(const MsmPlan& P, size_t short_terms, size_t full_terms);
 // edc_single.hip
 void launch_init_btable(hipStream_t st, uint32_t* btab);
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,

@@ -3,140 +3,151 @@
 // (reference src/batch.rs:205-210, EdwardsPoint::vartime_multiscalar_mul; any exact algorithm
 // yields the same group element).
 //
-// Points p: 0 = B, 1..n = R_i (128-bit z, 8 windows, top digit unsigned up to 2^16),
-//           n+1..n+m = distinct keys (253-bit, 16 signed windows); in few-key mode
-//           (edc_common.h) B and the keys carry 128-bit halves and their [2^128] twins follow,
-//           so every point has 8 windows.
-// Buckets: signed radix-2^16 digits d, bucket |d| in window w. A bin = (window, slice of 256
-// consecutive buckets) = one workgroup. Entries are binned by a count / scan / scatter pass
-// (LDS-aggregated histograms, no global sort), then each bin's workgroup counting-sorts its
-// entries in LDS, accumulates one bucket per lane with 7M mixed additions, and reduces its 256
-// buckets to (sum_t (t+1) S_t, sum_t S_t). Windows combine slices; a final Horner pass joins
-// windows, multiplies by the cofactor and tests the identity (src/batch.rs:212-216).
+// The windows, buckets and bins follow an MsmPlan (edc_common.h) chosen per batch on the host:
+// 128-bit z_i use the low windows only, full-width coefficients (B, keys) every window. Digits
+// are binned by (range, window, slice of 256 buckets) by a count / scan / scatter pass
+// (LDS-aggregated histograms, no global sort); each bin's workgroup counting-sorts its entries,
+// accumulates its buckets with 7M mixed additions (segmented lanes, LDS-DMA row gathers) and
+// reduces them to (sum_t (t+1) S_t, sum_t S_t). Windows with several slices combine them; a
+// Horner pass per range joins the windows, multiplies by the cofactor and tests the identity
+// (src/batch.rs:212-216). Ranges > 1 only in the grouped fallback: independent MSMs over
+// contiguous slices of the signatures, one verdict each.
 #include "edc_common.h"
 #include "edc_launch.h"
 #include "ge_quad.h"
 
 namespace edc {
 
-constexpr int CNT_PTS_PER_BLOCK = 4096;   // points per count/scatter workgroup
+constexpr int CNT_TERMS_PER_BLOCK = 4096;   // terms per count/scatter workgroup
 
-__device__ __forceinline__ void load_scalar(const uint32_t* scal, uint32_t p, uint32_t s[8]) {
-  const uint4* q = reinterpret_cast<const uint4*>(scal + (size_t)p * 8);
-  uint4 a = q[0], b = q[1];
+__device__ __forceinline__ uint32_t terms_count(const MsmTerms& T, const int* flags) {
+  return T.rsize ? T.npoint + T.nx : msm_num_points(T.n, (uint32_t)flags[FLAG_NKEYS]);
+}
+
+// term t -> point index, range, short scalar?, scalar words
+__device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t& pt, uint32_t& rg, bool& shrt,
+                                         uint32_t s[8]) {
+  const uint32_t* src;
+  if (!T.rsize) {
+    pt = t;
+    rg = 0;
+    shrt = t >= 1 && t <= T.n;
+    src = T.scal + (size_t)t * 8;
+  } else if (t < T.npoint) {       // R_i (t < n), then one key term per signature
+    pt = 1 + t;
+    rg = (t < T.n ? t : t - T.n) / T.rsize;
+    shrt = t < T.n;
+    src = T.scal + (size_t)pt * 8;
+  } else {                          // listed (range, key) and per-range B terms
+    const uint32_t q = t - T.npoint;
+    pt = T.xpt[q];
+    rg = T.xrg[q];
+    shrt = false;
+    src = T.xscal + (size_t)q * 8;
+  }
+  const uint4* q4 = reinterpret_cast<const uint4*>(src);
+  const uint4 a = q4[0], b = q4[1];
   s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
 }
 
-__global__ void __launch_bounds__(256) k_msm_count(uint32_t n, const uint32_t* __restrict__ scal,
-                                                   uint32_t* __restrict__ counts,
-                                                   const int* __restrict__ flags) {
-  __shared__ uint32_t hist[NBIN];
-  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
-  __syncthreads();
-  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  const bool few = few_key_mode(n, m);
-  const uint32_t npts = msm_num_points(n, m);
-  const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
-  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
-    uint32_t p = p0 + t;
-    if (p >= npts) break;
-    uint32_t s[8];
-    load_scalar(scal, p, s);
-    const bool isR = msm_short_scalar(p, n, few);
-    const int nwin = isR ? NWIN_Z : NWIN_FULL;
-    int carry = 0;
-    for (int w = 0; w < nwin; ++w) {
-      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
-      if (d) {
-        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-        atomicAdd(&hist[w * NSLICE + (b >> SLICE_BITS)], 1u);
-      }
+// digits of term t: calls f(bin, local bucket, negative) for every non-zero digit
+template <typename F>
+__device__ __forceinline__ void term_digits(const MsmPlan& P, bool shrt, uint32_t rg, const uint32_t s[8], F&& f) {
+  const uint32_t nw = shrt ? P.nwin_short : P.nwin;
+  const uint32_t rbase = rg * P.bins_per_range;
+  int carry = 0;
+  for (uint32_t w = 0; w < nw; ++w) {
+    const int d = plan_digit(s, P.off[w], P.bits[w], carry, shrt && w + 1 == nw);
+    if (d) {
+      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+      f(rbase + P.bin0[w] + (b >> SLICE_BITS), b & (NSLICE - 1), d < 0);
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32_t* __restrict__ counts,
+                                                   const int* __restrict__ flags) {
+  extern __shared__ uint32_t hist[];
+  const uint32_t nbin = P.nbin();
+  for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  for (int b = threadIdx.x; b < NBIN; b += blockDim.x)
+  const uint32_t cnt = terms_count(T, flags);
+  const uint32_t t0 = blockIdx.x * CNT_TERMS_PER_BLOCK;
+  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+    const uint32_t t = t0 + u;
+    if (t >= cnt) break;
+    uint32_t pt, rg, s[8];
+    bool shrt;
+    term_get(T, t, pt, rg, shrt, s);
+    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x)
     if (hist[b]) atomicAdd(&counts[b], hist[b]);
 }
 
-// exclusive scan of NBIN counts (one workgroup of 1024 lanes, 4 bins per lane)
-__global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ counts,
+// exclusive scan of nbin counts (one workgroup of 1024 lanes, consecutive bins per lane)
+__global__ void __launch_bounds__(1024) k_msm_scan(uint32_t nbin, const uint32_t* __restrict__ counts,
                                                    uint32_t* __restrict__ offsets,
                                                    uint32_t* __restrict__ cursor) {
   __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  uint32_t c[4], s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { c[j] = counts[4 * t + j]; s += c[j]; }
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nbin + 1023) / 1024;
+  const uint32_t b0 = t * per, b1 = min(nbin, b0 + per);
+  uint32_t s = 0;
+  for (uint32_t b = b0; b < b1; ++b) s += counts[b];
   part[t] = s;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
-    uint32_t v = t >= d ? part[t - d] : 0;
+    uint32_t v = t >= (uint32_t)d ? part[t - d] : 0;
     __syncthreads();
     part[t] += v;
     __syncthreads();
   }
   uint32_t run = part[t] - s;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    offsets[4 * t + j] = run;
-    cursor[4 * t + j] = run;
-    run += c[j];
+  for (uint32_t b = b0; b < b1; ++b) {
+    offsets[b] = run;
+    cursor[b] = run;
+    run += counts[b];
   }
 }
 
-__global__ void __launch_bounds__(256) k_msm_scatter(uint32_t n, const uint32_t* __restrict__ scal,
-                                                     uint32_t* __restrict__ cursor,
-                                                     uint2* __restrict__ entries,
-                                                     const int* __restrict__ flags) {
-  __shared__ uint32_t hist[NBIN];
-  __shared__ uint32_t gbase[NBIN];
-  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) hist[b] = 0;
+__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint32_t* __restrict__ cursor,
+                                                     uint2* __restrict__ entries, const int* __restrict__ flags) {
+  extern __shared__ uint32_t smem_hist[];
+  const uint32_t nbin = P.nbin();
+  uint32_t* hist = smem_hist;
+  uint32_t* gbase = smem_hist + nbin;
+  for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  const bool few = few_key_mode(n, m);
-  const uint32_t npts = msm_num_points(n, m);
-  const uint32_t p0 = blockIdx.x * CNT_PTS_PER_BLOCK;
-  // pass 1: local ranks (recomputed in pass 2 from the same digits)
-  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
-    uint32_t p = p0 + t;
-    if (p >= npts) break;
-    uint32_t s[8];
-    load_scalar(scal, p, s);
-    const bool isR = msm_short_scalar(p, n, few);
-    const int nwin = isR ? NWIN_Z : NWIN_FULL;
-    int carry = 0;
-    for (int w = 0; w < nwin; ++w) {
-      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
-      if (d) {
-        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-        atomicAdd(&hist[w * NSLICE + (b >> SLICE_BITS)], 1u);
-      }
-    }
+  const uint32_t cnt = terms_count(T, flags);
+  const uint32_t t0 = blockIdx.x * CNT_TERMS_PER_BLOCK;
+  // pass 1: local counts (recomputed in pass 2 from the same digits)
+  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+    const uint32_t t = t0 + u;
+    if (t >= cnt) break;
+    uint32_t pt, rg, s[8];
+    bool shrt;
+    term_get(T, t, pt, rg, shrt, s);
+    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < NBIN; b += blockDim.x) {
+  for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) {
     uint32_t c = hist[b];
     gbase[b] = c ? atomicAdd(&cursor[b], c) : 0u;
     hist[b] = 0;
   }
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < CNT_PTS_PER_BLOCK; t += blockDim.x) {
-    uint32_t p = p0 + t;
-    if (p >= npts) break;
-    uint32_t s[8];
-    load_scalar(scal, p, s);
-    const bool isR = msm_short_scalar(p, n, few);
-    const int nwin = isR ? NWIN_Z : NWIN_FULL;
-    int carry = 0;
-    for (int w = 0; w < nwin; ++w) {
-      int d = scalar_digit(s, w, carry, isR && w == NWIN_Z - 1);
-      if (d) {
-        uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-        uint32_t bin = w * NSLICE + (b >> SLICE_BITS);
-        uint32_t r = atomicAdd(&hist[bin], 1u);
-        entries[gbase[bin] + r] = make_uint2(p | (d < 0 ? 0x80000000u : 0u), b & (NSLICE - 1));
-      }
-    }
+  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+    const uint32_t t = t0 + u;
+    if (t >= cnt) break;
+    uint32_t pt, rg, s[8];
+    bool shrt;
+    term_get(T, t, pt, rg, shrt, s);
+    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t local, bool neg) {
+      const uint32_t r = atomicAdd(&hist[bin], 1u);
+      entries[gbase[bin] + r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local);
+    });
   }
 }
 
@@ -208,151 +219,7 @@ __device__ __forceinline__ ge_p3 sum_256(const ge_p3& mine, uint32_t* scratch) {
   return a;
 }
 
-constexpr int BKT_CHUNK = 4096;
-
-// one workgroup per bin (window w, slice s) of 256 buckets: S_b for b = 256 s + t + 1.
-// Entries are counting-sorted by local bucket in LDS (chunks of BKT_CHUNK). ACC_LANES lanes share
-// a bucket (lane group (t, t + 256, ...) walks entries j = half, half + ACC_LANES, ...; the group
-// is summed at the end), which shortens the serial chains of the dense bins. Bucket sizes are
-// Poisson-distributed and a wave runs as long as its fullest lane, so buckets are handed to lanes
-// in order of decreasing entry count. With ACC_PREFETCH the next Niels point is loaded under the
-// current 7M mixed addition.
-#ifndef EDC_ACC_LANES
-#define EDC_ACC_LANES 1
-#endif
-#ifndef EDC_ACC_PREFETCH
-#define EDC_ACC_PREFETCH 0
-#endif
-#ifndef EDC_ACC_WAVES
-#define EDC_ACC_WAVES 4
-#endif
-constexpr int ACC_LANES = EDC_ACC_LANES;
-constexpr int ACC_THREADS = ACC_LANES * NSLICE;
-
-__global__ void __launch_bounds__(ACC_THREADS, EDC_ACC_WAVES) k_msm_accum(const uint32_t* __restrict__ counts,
-                                                              const uint32_t* __restrict__ offsets,
-                                                              const uint2* __restrict__ entries,
-                                                              const uint32_t* __restrict__ pts,
-                                                              uint32_t* __restrict__ buckets) {
-  __shared__ uint32_t lidx[BKT_CHUNK];
-  __shared__ uint32_t lcnt[NSLICE];
-  __shared__ uint32_t lstart[NSLICE];
-  __shared__ uint32_t lcur[NSLICE];
-  __shared__ uint32_t lorder[NSLICE];   // bucket handled by lane group t (by decreasing count)
-#if EDC_ACC_LANES > 1
-  __shared__ __attribute__((aligned(16))) uint32_t lpart[NSLICE * EXT_WORDS];
-#endif
-  const int t = threadIdx.x;
-  const int lane_b = t & (NSLICE - 1);  // bucket slot of this lane group
-  const uint32_t half = (uint32_t)t >> 8;
-  const uint32_t bin = blockIdx.x;
-  const uint32_t E = counts[bin];
-  if (E == 0) return;
-  const uint32_t off = offsets[bin];
-  ge_p3 acc = ge_identity();
-  uint32_t my_bucket = lane_b;
-  for (uint32_t c0 = 0; c0 < E; c0 += BKT_CHUNK) {
-    const uint32_t ch = min((uint32_t)BKT_CHUNK, E - c0);
-    if (t < NSLICE) lcnt[t] = 0;
-    __syncthreads();
-    for (uint32_t e = t; e < ch; e += ACC_THREADS) atomicAdd(&lcnt[entries[off + c0 + e].y], 1u);
-    __syncthreads();
-    if (t < 64) {
-      uint32_t c[4], s = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { c[j] = lcnt[4 * t + j]; s += c[j]; }
-      uint32_t incl = s;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        uint32_t v = __shfl_up(incl, d, 64);
-        if (t >= d) incl += v;
-      }
-      uint32_t run = incl - s;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { lstart[4 * t + j] = run; lcur[4 * t + j] = run; run += c[j]; }
-    }
-    if (c0 == 0 && t >= ACC_THREADS - NSLICE) {
-      // rank bucket b by (count desc, index)
-      const int b = t - (ACC_THREADS - NSLICE);
-      const uint32_t mine = lcnt[b];
-      uint32_t rank = 0;
-      for (int u = 0; u < NSLICE; ++u) {
-        const uint32_t o = lcnt[u];
-        rank += (o > mine) || (o == mine && u < b);
-      }
-      lorder[rank] = b;
-    }
-    __syncthreads();
-    if (c0 == 0) my_bucket = lorder[lane_b];
-    for (uint32_t e = t; e < ch; e += ACC_THREADS) {
-      uint2 en = entries[off + c0 + e];
-      uint32_t pos = atomicAdd(&lcur[en.y], 1u);
-      lidx[pos] = en.x;
-    }
-    __syncthreads();
-    const uint32_t beg = lstart[my_bucket], cnt = lcnt[my_bucket];
-#if EDC_ACC_PREFETCH
-    if (half < cnt) {
-      uint32_t e = lidx[beg + half];
-      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-      for (uint32_t j = half; j < cnt; j += ACC_LANES) {
-        const uint32_t e_next = (j + ACC_LANES < cnt) ? lidx[beg + j + ACC_LANES] : e;
-        ge_niels q_next = ld_niels(pts, e_next & 0x7FFFFFFFu);
-        if (e >> 31) q = ge_niels_neg(q);
-        acc = ge_madd(acc, q);
-        e = e_next;
-        q = q_next;
-      }
-    }
-#else
-#if EDC_ACC_PROBE == 3      // measurement probe: LDS sort only, no accumulation (result wrong)
-    if (cnt > 100000) acc.X.v[0] = lidx[beg];
-#elif EDC_ACC_PROBE == 4    // measurement probe: accumulate unsorted entries straight from HBM
-    for (uint32_t j = t; j < ch; j += ACC_THREADS) {
-      const uint32_t e = entries[off + c0 + j].x;
-      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-      if (e >> 31) q = ge_niels_neg(q);
-      acc = ge_madd(acc, q);
-    }
-#else
-    for (uint32_t j = half; j < cnt; j += ACC_LANES) {
-      const uint32_t e = lidx[beg + j];
-#endif
-#if EDC_ACC_PROBE == 3 || EDC_ACC_PROBE == 4
-    for (uint32_t j = 0; j < 0; ++j) {
-      const uint32_t e = 0;
-#endif
-#if EDC_ACC_PROBE == 1      // measurement probe: gathers + sort only (result wrong)
-      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc.X.v[k] ^= q.ypx.v[k] ^ q.ymx.v[k] ^ q.xy2d.v[k];
-#elif EDC_ACC_PROBE == 2    // measurement probe: arithmetic only, no gather (result wrong)
-      ge_niels q = ld_niels(pts, 1 + (e & 1));
-      if (e >> 31) q = ge_niels_neg(q);
-      acc = ge_madd(acc, q);
-#else
-      ge_niels q = ld_niels(pts, e & 0x7FFFFFFFu);
-      if (e >> 31) q = ge_niels_neg(q);
-      acc = ge_madd(acc, q);
-#endif
-    }
-#endif
-    __syncthreads();
-  }
-#if EDC_ACC_LANES > 1
-  if (half) st_ext(lpart + lane_b * EXT_WORDS, acc);
-  __syncthreads();
-  if (half) return;
-  acc = ge_add(acc, ld_ext(lpart + lane_b * EXT_WORDS));
-#endif
-  st_ext(buckets + ((size_t)bin * NSLICE + my_bucket) * EXT_WORDS, acc);
-}
-
-#ifndef EDC_ACC_DMA
-#define EDC_ACC_DMA 1
-#endif
-
-// ---- bucket accumulation with coalesced row gathers (EDC_ACC_DMA) ----
+// ---- bucket accumulation with coalesced row gathers ----
 // One workgroup per bin, one lane per bucket (buckets handed to lanes by decreasing entry count,
 // so the lanes of a wave run about the same number of rounds). The bin's entries are counting-
 // sorted by bucket through LDS counters into `sorted` (global, so a bin of any size is sorted in
@@ -397,7 +264,7 @@ __device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin
   return buckets + ((size_t)bin * NSLICE + b) * EXT_WORDS;
 }
 
-__global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint32_t* __restrict__ counts,
+__global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __restrict__ counts,
                                                                    const uint32_t* __restrict__ offsets,
                                                                    const uint2* __restrict__ entries,
                                                                    uint32_t* __restrict__ sorted,
@@ -486,15 +353,6 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
   }
   // one round of row gathers: the wave's 64 rows (one per lane, `row`) -> wrows, row-major
   auto gather_rows = [&](uint32_t row) {
-#if EDC_ACC_PROBE == 5      // measurement probe: 64-byte rows (4 pieces, 4 DMA instructions)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t g = 64u * k + lane;
-      const uint32_t r = (uint32_t)__shfl((int)row, (int)(g >> 2), 64);
-      dma_piece(pts + (size_t)r * NIELS_WORDS + (g & 3) * 4, wrows + k * 256);
-    }
-    return;
-#endif
     asm volatile("" : "+v"(pmap0), "+v"(pmap1));   // unpacked each round, never hoisted (VGPRs)
 #pragma unroll
     for (int k = 0; k < ROW_PIECES; ++k) {
@@ -507,9 +365,7 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
   // software pipeline: the rows of round j + 1 are in flight while round j's addition runs
   uint32_t e = lo < hi ? sorted[off + lo] : 0u;
   uint32_t e_next = lo + 1 < hi ? sorted[off + lo + 1] : e;
-#if EDC_ACC_PROBE != 2 && EDC_ACC_PROBE != 6
   gather_rows(e & 0x7FFFFFFFu);
-#endif
   for (uint32_t j = 0; j < rounds; ++j) {
     const uint32_t pos = lo + j;
     if (pos < hi && pos == cend) {                 // the running bucket ended: flush it
@@ -519,25 +375,16 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
       do { ++cb; } while (lend[cb] <= pos);        // skip empty buckets
       cend = lend[cb];
     }
-#if EDC_ACC_PROBE == 2 || EDC_ACC_PROBE == 6   // measurement probes: no gather (result wrong)
-    ge_niels q = ld_niels(pts, 1 + (e & 1));
-#else
     __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): round j's rows are in LDS
     ge_niels q = ld_row_lds(wrows + lane * ROW_WORDS);
     __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): row in VGPRs before the refill
     if (j + 1 < rounds) gather_rows(e_next & 0x7FFFFFFFu);   // lanes past their range re-read a row
-#endif
     const uint32_t e_cur = e;
     e = e_next;
     if (pos + 2 < hi) e_next = sorted[off + pos + 2];
     if (pos < hi) {
-#if EDC_ACC_PROBE == 1 || EDC_ACC_PROBE == 5 || EDC_ACC_PROBE == 6   // probes: no addition (result wrong)
-#pragma unroll
-      for (int k = 0; k < 9; ++k) acc.X.v[k] ^= q.ypx.v[k] ^ q.ymx.v[k] ^ q.xy2d.v[k];
-#else
       if (e_cur >> 31) q = ge_niels_neg(q);
       acc = ge_madd(acc, q);
-#endif
     }
   }
   // the open segment: a head partial, a whole bucket ending at hi, or the first part of a bucket
@@ -571,59 +418,28 @@ __global__ void __launch_bounds__(256, EDC_ACC_WAVES) k_msm_accum_dma(const uint
   }
 }
 
-// one workgroup per bin: W_s = sum_t (t+1) S_t and T_s = sum_t S_t (quad-cooperative)
-__global__ void __launch_bounds__(256) k_msm_reduce(const uint32_t* __restrict__ counts,
-                                                    const uint32_t* __restrict__ buckets,
-                                                    uint32_t* __restrict__ slice_W,
-                                                    uint32_t* __restrict__ slice_T) {
+// Win(range g, window w) = sum_s W_s + 256 * sum_s s T_s over the window's slices (windows with
+// more than one slice; they form a prefix of the plan). One workgroup per (range, window).
+__global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, uint32_t nmulti, const uint32_t* __restrict__ slice_W,
+                                                    const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __builtin_amdgcn_s_setprio(3);   // latency-bound tail: issue ahead of co-resident bulk waves
   const int t = threadIdx.x;
-  const uint32_t bin = blockIdx.x;
-  if (counts[bin] == 0) {
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
-    }
-    return;
-  }
+  const uint32_t g = blockIdx.x / nmulti, w = blockIdx.x % nmulti;
+  const uint32_t ns = P.nslice[w];
+  const uint32_t b0 = g * P.bins_per_range + P.bin0[w];
   uint32_t* lpts = smem;
-  st_ext(lpts + t * EXT_WORDS, ld_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS));
-  __syncthreads();
-  ge_p3 ws, tot;
-  weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
-  if (t < 4) {
-    ge_p3 W = quad_add(ws, tot);       // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
-    }
-  }
-}
-
-// one workgroup per window: Win_w = sum_s W_s + 256 * sum_s s T_s
-// (a window without entries -- windows 8..15 in few-key mode -- is skipped; FLAG_WINMASK records
-// the non-empty ones for the Horner pass)
-__global__ void __launch_bounds__(256) k_msm_window(const uint32_t* __restrict__ counts,
-                                                    const uint32_t* __restrict__ slice_W,
-                                                    const uint32_t* __restrict__ slice_T,
-                                                    uint32_t* __restrict__ win, int* __restrict__ flags) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const int t = threadIdx.x;
-  const uint32_t w = blockIdx.x;
-  if (!__syncthreads_or(counts[w * NSLICE + t] != 0)) return;
-  if (t == 0) atomicOr(&flags[FLAG_WINMASK], 1 << w);
-  uint32_t* lpts = smem;
-  st_ext(lpts + t * EXT_WORDS, ld_ext(slice_T + (size_t)(w * NSLICE + t) * EXT_WORDS));
+  st_ext(lpts + t * EXT_WORDS, (uint32_t)t < ns ? ld_ext(slice_T + (size_t)(b0 + t) * EXT_WORDS) : ge_identity());
   __syncthreads();
   ge_p3 ws, tot;
   weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
   __syncthreads();
-  ge_p3 a = sum_256(ld_ext(slice_W + (size_t)(w * NSLICE + t) * EXT_WORDS), lpts);
+  ge_p3 a = sum_256((uint32_t)t < ns ? ld_ext(slice_W + (size_t)(b0 + t) * EXT_WORDS) : ge_identity(), lpts);
   if (t < 4) {
     ge_p3 x = ws;
-    for (int k = 0; k < 8; ++k) x = quad_dbl(x);
+    for (int k = 0; k < SLICE_BITS; ++k) x = quad_dbl(x);
     ge_p3 r = quad_add(a, x);
-    if (t == 0) st_ext(win + (size_t)w * EXT_WORDS, r);
+    if (t == 0) st_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS, r);
   }
 }
 
@@ -676,20 +492,29 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
   }
 }
 
-// Horner over windows on one quad (4 cooperating lanes), then x8 / identity / optional
-// compression (single lane; only when the caller asked for check8).
-__global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restrict__ flags,
-                            int want_compress, uint8_t* __restrict__ out) {
-  if (threadIdx.x >= 4 || blockIdx.x != 0) return;
-  // Horner from the highest non-empty window (windows without entries were never written)
-  const uint32_t mask = (uint32_t)flags[FLAG_WINMASK];
-  const int top = mask ? 31 - __builtin_clz(mask) : -1;
-  ge_p3 acc = ge_identity();
-  for (int w = top; w >= 0; --w) {
-    if (w != top)
-      for (int k = 0; k < WIN_BITS; ++k) acc = quad_dbl(acc);
-    if (mask & (1u << w)) acc = quad_add(acc, ld_ext(win + (size_t)w * EXT_WORDS));
+// window sum of (range g, window w): combined by k_msm_window, or the single bin's W
+__device__ __forceinline__ ge_p3 window_sum(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* slice_W,
+                                             const uint32_t* win) {
+  if (P.nslice[w] > 1) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
+  return ld_ext(slice_W + (size_t)(g * P.bins_per_range + P.bin0[w]) * EXT_WORDS);
+}
+
+// Horner over the windows of range g on one quad (4 cooperating lanes): sum_w 2^off[w] Win_w
+__device__ __forceinline__ ge_p3 horner(const MsmPlan& P, uint32_t g, const uint32_t* slice_W, const uint32_t* win) {
+  ge_p3 acc = window_sum(P, g, P.nwin - 1, slice_W, win);
+  for (int w = (int)P.nwin - 2; w >= 0; --w) {
+    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = quad_dbl(acc);
+    acc = quad_add(acc, window_sum(P, g, (uint32_t)w, slice_W, win));
   }
+  return acc;
+}
+
+// batch: Horner, x8, identity (requires Z != 0), optional compression, partial point
+__global__ void k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W, const uint32_t* __restrict__ win,
+                            const int* __restrict__ flags, int want_compress, uint8_t* __restrict__ out) {
+  if (threadIdx.x >= 4 || blockIdx.x != 0) return;
+  __builtin_amdgcn_s_setprio(3);   // a serial chain: issue ahead of co-resident bulk waves
+  const ge_p3 acc = horner(P, 0, slice_W, win);
   ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
   if (threadIdx.x != 0) return;
   ext_to_canonical_bytes(acc, out + 48);
@@ -697,12 +522,25 @@ __global__ void k_msm_final(const uint32_t* __restrict__ win, const int* __restr
   reinterpret_cast<int*>(out)[0] = (!bad && ge_is_identity(c8)) ? 0 : 1;
   reinterpret_cast<int*>(out)[1] = bad;
   reinterpret_cast<int*>(out)[2] = flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
+  reinterpret_cast<int*>(out)[3] = flags[FLAG_OVF];
   if (want_compress) {
     uint32_t w8[8];
     ge_compress(c8, w8);
     for (int j = 0; j < 8; ++j)
       for (int b = 0; b < 4; ++b) out[16 + 4 * j + b] = (uint8_t)(w8[j] >> (8 * b));
   }
+}
+
+// ranges: rverdict[g] = 0 iff [8] * (range g's check point) is the identity; one quad per range
+__global__ void __launch_bounds__(64) k_msm_range_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
+                                                        const uint32_t* __restrict__ win,
+                                                        uint8_t* __restrict__ rverdict) {
+  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;   // a quad never straddles the bound
+  if (g >= P.nranges) return;
+  __builtin_amdgcn_s_setprio(3);
+  const ge_p3 acc = horner(P, g, slice_W, win);
+  const ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
+  if ((threadIdx.x & 3) == 0) rverdict[g] = ge_is_identity(c8) ? 0 : 1;
 }
 
 // combine G partial check points (canonical 128-byte records) from G shards
@@ -717,40 +555,49 @@ __global__ void k_combine(uint32_t g, const uint8_t* __restrict__ partials, int 
 // ---------------------------------------------------------------- launchers
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
-void launch_msm_bin(hipStream_t st, uint32_t n, const uint32_t* scal, uint32_t* counts,
+void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags) {
-  const uint32_t maxpts = 1 + 2 * n;
-  (void)hipMemsetAsync(counts, 0, NBIN * sizeof(uint32_t), st);
-  hipLaunchKernelGGL(k_msm_count, dim3(cdiv(maxpts, CNT_PTS_PER_BLOCK)), dim3(256), 0, st, n, scal, counts,
+  const uint32_t nbin = P.nbin();
+  (void)hipMemsetAsync(counts, 0, nbin * sizeof(uint32_t), st);
+  const uint32_t grid = cdiv(max_terms ? max_terms : 1, CNT_TERMS_PER_BLOCK);
+  hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, counts, flags);
+  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
+  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), 2 * nbin * sizeof(uint32_t), st, P, T, cursor, entries,
                      flags);
-  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, counts, offsets, cursor);
-  hipLaunchKernelGGL(k_msm_scatter, dim3(cdiv(maxpts, CNT_PTS_PER_BLOCK)), dim3(256), 0, st, n, scal,
-                     cursor, entries, flags);
 }
 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
 
-void launch_msm_bucket(hipStream_t st, const uint32_t* counts, const uint32_t* offsets,
+void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
                        uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
-#if EDC_ACC_DMA
-  hipLaunchKernelGGL(k_msm_accum_dma, dim3(NBIN), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
+  // one workgroup per bin; the bin reduction is fused into the accumulation
+  hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
                      heads, slice_W, slice_T);
-  return;                              // the reduction is fused into the accumulation
-#else
-  (void)sorted;
-  (void)heads;
-  hipLaunchKernelGGL(k_msm_accum, dim3(NBIN), dim3(ACC_THREADS), 0, st, counts, offsets, entries, pts, buckets);
-#endif
-  hipLaunchKernelGGL(k_msm_reduce, dim3(NBIN), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
 }
 
-size_t msm_bucket_words() { return (size_t)NBIN * NSLICE * EXT_WORDS; }
+size_t msm_bucket_words(uint32_t nbin) { return (size_t)nbin * NSLICE * EXT_WORDS; }
 
-void launch_msm_tail(hipStream_t st, const uint32_t* counts, const uint32_t* slice_W, const uint32_t* slice_T,
+static uint32_t plan_nmulti(const MsmPlan& P) {
+  uint32_t k = 0;
+  while (k < P.nwin && P.nslice[k] > 1) ++k;
+  return k;
+}
+
+void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out) {
-  hipLaunchKernelGGL(k_msm_window, dim3(NWIN_FULL), dim3(256), kReduceLds, st, counts, slice_W, slice_T, win, flags);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, win, flags, want_compress, out);
+  const uint32_t nm = plan_nmulti(P);
+  if (nm) hipLaunchKernelGGL(k_msm_window, dim3(nm), dim3(256), kReduceLds, st, P, nm, slice_W, slice_T, win);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, P, slice_W, win, flags, want_compress, out);
+}
+
+void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
+                           uint32_t* win, uint8_t* rverdict) {
+  const uint32_t nm = plan_nmulti(P);
+  if (nm)
+    hipLaunchKernelGGL(k_msm_window, dim3(nm * P.nranges), dim3(256), kReduceLds, st, P, nm, slice_W, slice_T, win);
+  hipLaunchKernelGGL(k_msm_range_final, dim3(cdiv(4ull * P.nranges, 64)), dim3(64), 0, st, P, slice_W, win,
+                     rverdict);
 }
 
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
@@ -758,6 +605,9 @@ void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad
   hipLaunchKernelGGL(k_combine, dim3(1), dim3(64), 0, st, g, partials, bad, want_compress, out);
 }
 
-size_t msm_entry_capacity(uint32_t n) { return (size_t)NWIN_Z * n + (size_t)NWIN_FULL * (n + 1); }
+// entries of a plan: every term can put one digit in each of its windows
+size_t msm_entry_capacity(const MsmPlan& P, size_t short_terms, size_t full_terms) {
+  return (size_t)P.nwin_short * short_terms + (size_t)P.nwin * full_terms;
+}
 
 }  // namespace edc

@@ -57,23 +57,11 @@ __global__ void __launch_bounds__(SHA_THREADS, 4) k_challenge(uint32_t n, const 
   kp[1] = make_uint4(k.v[4], k.v[5], k.v[6], k.v[7]);
 }
 
-// ZIP215 decode of every signature's R_i -> points[1 + i] (affine Niels).
-#ifndef EDC_DEC_WAVES
-#define EDC_DEC_WAVES 4
-#endif
-__global__ void __launch_bounds__(256, EDC_DEC_WAVES) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
-                                                       uint32_t* __restrict__ pts, int* __restrict__ flags) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t w[8];
-  ld_words8(sig + (size_t)i * 64, w);
-  ge_p3 P;
-  const bool ok = ge_decompress(w, P);
-  st_niels(pts, 1 + i, ge_to_niels_affine(P));
-  if (!ok) atomicOr(&flags[FLAG_BAD], 1);
-}
-
-// one 128-byte Niels record src -> pts[idx]
+// ZIP215 decode (K2) of every signature's R_i -> points[1 + i] and of every distinct key j (its
+// first signature's raw bytes, src/batch.rs:183-185) -> points[1 + n + j], in ONE launch: lanes
+// [0, n) decode R_i, lanes [n, n + m) decode the keys (m is read on the device; surplus lanes
+// exit). Keys registered in the context's cache copy their decoded record instead. Per-item and
+// per-key failure bits are kept for the grouped fallback.
 __device__ __forceinline__ void copy_record(uint32_t* __restrict__ pts, uint32_t idx, const uint32_t* __restrict__ src) {
   const uint4* q = reinterpret_cast<const uint4*>(src);
   uint4* d = reinterpret_cast<uint4*>(pts + (size_t)idx * NIELS_WORDS);
@@ -81,87 +69,63 @@ __device__ __forceinline__ void copy_record(uint32_t* __restrict__ pts, uint32_t
   for (int i = 0; i < NIELS_WORDS / 4; ++i) d[i] = q[i];
 }
 
-// Side stream, concurrent with k_decompress: ZIP215 decode of each distinct key j (its first
-// signature's raw bytes, src/batch.rs:183-185) -> points[1 + n + j].
-__global__ void __launch_bounds__(256, 4) k_key_points(uint32_t n, const uint8_t* __restrict__ vk,
-                                                       const uint32_t* __restrict__ key_rep,
-                                                       uint32_t* __restrict__ pts, int* __restrict__ flags,
+__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
+                                                       const uint8_t* __restrict__ vk,
+                                                       const uint32_t* __restrict__ key_rep, int per_sig_host,
+                                                       uint32_t* __restrict__ pts, uint8_t* __restrict__ itembad,
+                                                       uint8_t* __restrict__ keybad, int* __restrict__ flags,
                                                        KeyCacheView kcache) {
-  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  // grid-stride (any grid size is correct)
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
-    uint32_t w[8];
-    ld_words8(vk + (size_t)(key_rep ? key_rep[j] : j) * 32, w);
-    const int ci = kc_lookup(kcache, w);
-    if (ci >= 0) {                  // registered key: A = comb[0][0], decoded once per context
-      copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
-      if (!kcache.ok[ci]) atomicOr(&flags[FLAG_BAD], 1);
-      continue;
-    }
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t w[8];
+  if (i < n) {
+    ld_words8(sig + (size_t)i * 64, w);
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
-    st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
-    if (!ok) atomicOr(&flags[FLAG_BAD], 1);
-  }
-}
-
-// 1/2 mod p: affine (x, y) back from a Niels record, x = (ypx - ymx)/2, y = (ypx + ymx)/2
-__device__ __forceinline__ fe fe_inv2() {
-  return fe_const(0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu,
-                  0xffffffffu, 0x3fffffffu);
-}
-
-// Few-key mode only (side stream, after k_key_points): [2^128]A_j as affine Niels at
-// points[1 + n + m + j], one quad of lanes per key (quad-cooperative doublings, ge_quad.h), and
-// the context constant [2^128]B copied to points[n + 2m + 1].
-__global__ void __launch_bounds__(64) k_key_shift(uint32_t n, const uint8_t* __restrict__ vk,
-                                                  const uint32_t* __restrict__ key_rep, uint32_t* __restrict__ pts,
-                                                  const uint32_t* __restrict__ bshift,
-                                                  const int* __restrict__ flags, KeyCacheView kcache) {
-  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  if (!few_key_mode(n, m)) return;
-  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t0 < NIELS_WORDS) pts[(size_t)(n + 2 * m + 1) * NIELS_WORDS + t0] = bshift[t0];
-  // grid-stride over quads (the stride is a multiple of 4, so a quad stays together)
-  for (uint32_t t = t0; (t >> 2) < m; t += gridDim.x * blockDim.x) {
-    const uint32_t j = t >> 2;
-    if (kcache.table) {               // registered key: [2^128]A = comb[32][0]
-      uint32_t w[8];
-      ld_words8(vk + (size_t)(key_rep ? key_rep[j] : j) * 32, w);
-      const int ci = kc_lookup(kcache, w);
-      if (ci >= 0) {
-        if ((t & 3) == 0)
-          copy_record(pts, 1 + n + m + j, kcache.comb + ((size_t)ci * COMB_ENTRIES + COMB_SHIFT128) * NIELS_WORDS);
-        continue;
-      }
+    st_niels(pts, 1 + i, ge_to_niels_affine(P));
+    if (!ok) {
+      itembad[i] |= ITEM_BAD_R;
+      atomicOr(&flags[FLAG_BAD], 1);
     }
-    const ge_niels a = ld_niels(pts, 1 + n + j);
-    ge_p3 P;
-    P.X = fe_mul(fe_sub(a.ypx, a.ymx), fe_inv2());
-    P.Y = fe_mul(fe_add(a.ypx, a.ymx), fe_inv2());
-    P.Z = fe_one();
-    P.T = fe_mul(P.X, P.Y);
-    for (int k = 0; k < 128; ++k) P = quad_dbl(P);
-    const fe zi = fe_invert(P.Z);     // every lane of the quad holds the same point
-    ge_p3 Q;
-    Q.X = fe_mul(P.X, zi);
-    Q.Y = fe_mul(P.Y, zi);
-    Q.Z = fe_one();
-    Q.T = fe_mul(Q.X, Q.Y);
-    if ((t & 3) == 0) st_niels(pts, 1 + n + m + j, ge_to_niels_affine(Q));
+    return;
   }
+  const uint32_t j = i - n;
+  if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
+  const bool per_sig = per_sig_host || flags[FLAG_OVF];
+  ld_words8(vk + (size_t)(per_sig ? j : key_rep[j]) * 32, w);
+  const int ci = kc_lookup(kcache, w);
+  bool ok;
+  if (ci >= 0) {                    // registered key: A = comb[0][0], decoded once per context
+    copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
+    ok = kcache.ok[ci] != 0;
+  } else {
+    ge_p3 P;
+    ok = ge_decompress(w, P);
+    st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
+  }
+  keybad[j] = ok ? 0 : 1;
+  if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
 
-__device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t salt) {
-  uint32_t h = salt ^ 0x9E3779B9u;
+// Slot hash of the raw key bytes under a 64-bit per-context secret (drawn from OS randomness
+// when the context is created, re-mixed per batch): callers cannot aim chosen keys at one slot
+// without it. Probing is additionally capped (KEY_PROBE_CAP): a batch whose keys still collide
+// switches to one key term per signature (FLAG_OVF), which is the same group element, so
+// adversarial keys cost at most the distinct-key path.
+constexpr uint32_t KEY_PROBE_CAP = 64;
+__device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t s0, uint32_t s1) {
+  uint32_t h = s0 ^ 0x9E3779B9u, g = s1 ^ 0x7F4A7C15u;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     h ^= w[j];
     h *= 0x85EBCA6Bu;
     h ^= h >> 13;
+    g += w[j] ^ h;
+    g *= 0xC2B2AE35u;
+    g ^= g >> 16;
   }
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
+  h ^= (g << 11) | (g >> 21);
+  h *= 0x27D4EB2Fu;
+  h ^= h >> 15;
   return h;
 }
 
@@ -170,7 +134,8 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t salt)
 // stale relaxed read is safe). The claimer also draws the dense key index.
 __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* __restrict__ vk,
                                                     uint32_t* __restrict__ table, uint32_t tmask,
-                                                    uint32_t salt, uint32_t* __restrict__ slot_key,
+                                                    uint32_t salt0, uint32_t salt1, uint32_t probe_cap,
+                                                    uint32_t* __restrict__ slot_key,
                                                     uint32_t* __restrict__ key_slot_of_sig,
                                                     uint32_t* __restrict__ key_rep,
                                                     unsigned long long* __restrict__ key_acc,
@@ -179,8 +144,8 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
   if (i >= n) return;
   uint32_t w[8];
   ld_words8(vk + (size_t)i * 32, w);
-  uint32_t h = key_hash(w, salt) & tmask;
-  for (uint32_t probe = 0; probe <= tmask; ++probe) {
+  uint32_t h = key_hash(w, salt0, salt1) & tmask;
+  for (uint32_t probe = 0; probe < probe_cap; ++probe) {
     // plain (L1-cached) first probe: a slot never changes once claimed, and a stale EMPTY is
     // resolved by the CAS below, so the hot validator slots are served from L1
     uint32_t cur = __hip_atomic_load(&table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -217,22 +182,29 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
     }
     h = (h + 1) & tmask;
   }
+  atomicOr(&flags[FLAG_OVF], 1);    // give up grouping for this batch (see KEY_PROBE_CAP)
 }
 
+// dense key index per signature; after a probe overflow the batch falls back to one key term
+// per signature (m = n), decided here on the device
 __global__ void __launch_bounds__(256) k_key_index(uint32_t n, const uint32_t* __restrict__ key_slot_of_sig,
                                                    const uint32_t* __restrict__ slot_key,
-                                                   uint32_t* __restrict__ key_index) {
+                                                   uint32_t* __restrict__ key_index, int* __restrict__ flags) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (flags[FLAG_OVF]) {
+    if (i == 0) flags[FLAG_NKEYS] = (int)n;
+    return;
+  }
   key_index[i] = slot_key[key_slot_of_sig[i]];
 }
 
 struct seed8 { uint32_t w[8]; };
 
 constexpr int COEF_SIGS_PER_THREAD = 8;             // two ChaCha blocks -> z for 8 signatures
-constexpr int COEF_CHUNK = 256 * COEF_SIGS_PER_THREAD;
 constexpr int COEF_SLOTS = 256;                     // LDS key-accumulator slots
 constexpr int PL = 12;                              // limbs of a 128 x 256-bit product
+static_assert(COEF_CHUNK == 256 * COEF_SIGS_PER_THREAD, "k_coef chunk (edc_common.h)");
 
 // r[0..11] = z (4 limbs) * s (8 limbs), exact
 __device__ __forceinline__ void mul_128x256(const uint32_t z[4], const uint32_t s[8], uint32_t r[PL]) {
@@ -257,6 +229,9 @@ __device__ __forceinline__ void mul_128x256(const uint32_t z[4], const uint32_t 
 // 64-bit accumulators (per thread in registers for sum z*s, per key through LDS slots / global
 // 64-bit atomics for sum z*k) and reduced mod l once (k_key_final). Integer sums are
 // order-independent, so any schedule gives bit-identical coefficients.
+// Range mode (rsize > 0, grouped fallback): the sums are kept per (range, key) pair, index
+// (i / rsize) * m + key, and per range for z*s (rsize is a multiple of COEF_CHUNK, so a workgroup
+// never straddles two ranges).
 __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restrict__ sig,
                                               const uint32_t* __restrict__ kscal,
                                               const uint8_t* __restrict__ zexp, seed8 seed,
@@ -264,10 +239,12 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               uint32_t* __restrict__ scal,
                                               unsigned long long* __restrict__ key_acc,
                                               unsigned long long* __restrict__ u_acc,
-                                              int* __restrict__ flags, int per_sig) {
+                                              uint8_t* __restrict__ itembad,
+                                              int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
+  const bool per_sig = per_sig_host || flags[FLAG_OVF];
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
     tag[s] = 0xFFFFFFFFu;
 #pragma unroll
@@ -279,6 +256,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
   for (int j = 0; j < PL; ++j) ua[j] = 0;
   bool bad = false;
   const uint32_t base = blockIdx.x * COEF_CHUNK;
+  const uint32_t pair0 = rsize ? (base / rsize) * m : 0u;
   for (int grp = 0; grp < COEF_SIGS_PER_THREAD / 4; ++grp) {
     const uint32_t i0 = base + 4 * (threadIdx.x + 256 * grp);
     if (i0 >= n) break;
@@ -308,7 +286,9 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
       const uint4* kp = reinterpret_cast<const uint4*>(kscal + (size_t)i * 8);
       uint4 k0 = kp[0], k1 = kp[1];
       kw[0] = k0.x; kw[1] = k0.y; kw[2] = k0.z; kw[3] = k0.w; kw[4] = k1.x; kw[5] = k1.y; kw[6] = k1.z; kw[7] = k1.w;
-      bad |= !sc_is_canonical(sw);
+      const bool s_bad = !sc_is_canonical(sw);
+      bad |= s_bad;
+      if (!rsize) itembad[i] = s_bad ? ITEM_BAD_S : 0;   // first writer of the batch's per-item bits
       uint32_t u[PL], v[PL];
       mul_128x256(z, sw, u);
       mul_128x256(z, kw, v);
@@ -327,7 +307,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
         ap[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
         continue;
       }
-      const uint32_t key = key_index[i];
+      const uint32_t key = pair0 + key_index[i];
       const uint32_t slot = key & (COEF_SLOTS - 1);
       const uint32_t prev = atomicCAS(&tag[slot], 0xFFFFFFFFu, key);
       if (prev == 0xFFFFFFFFu || prev == key) {
@@ -356,7 +336,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
   __syncthreads();
   if (threadIdx.x < PL) {
     unsigned long long x = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(&u_acc[threadIdx.x], x);
+    atomicAdd(&u_acc[(rsize ? (size_t)(base / rsize) * PL : 0) + threadIdx.x], x);
   }
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
     const uint32_t key = tag[s];
@@ -382,36 +362,56 @@ __device__ __forceinline__ sc reduce_limb_sums(const unsigned long long* L) {
   return sc_reduce_wide(x);
 }
 
-// coefficient c of point p; in few-key mode c_lo goes to p and c_hi to its [2^128]-shifted twin
-__device__ __forceinline__ void store_coeff(uint32_t* scal, uint32_t p, uint32_t p_shift, const sc& c, bool few) {
-  uint4* d = reinterpret_cast<uint4*>(scal + (size_t)p * 8);
+__device__ __forceinline__ void store_scalar(uint32_t* scal, size_t idx, const sc& c) {
+  uint4* d = reinterpret_cast<uint4*>(scal + idx * 8);
   d[0] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
-  if (few) {
-    d[1] = make_uint4(0, 0, 0, 0);
-    uint4* h = reinterpret_cast<uint4*>(scal + (size_t)p_shift * 8);
-    h[0] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
-    h[1] = make_uint4(0, 0, 0, 0);
-  } else {
-    d[1] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
-  }
+  d[1] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
 }
 
+// Batch: A_coeff of key j = sum z k mod l -> scalar of point n+1+j; B_coeff = -sum z s -> point 0.
 __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned long long* __restrict__ key_acc,
                                                    const unsigned long long* __restrict__ u_acc,
                                                    uint32_t* __restrict__ scal,
-                                                   const int* __restrict__ flags, int per_sig) {
+                                                   const int* __restrict__ flags, int per_sig_host) {
   const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  const bool few = few_key_mode(n, m);
-  for (uint32_t j = j0; j < (per_sig ? 0u : m); j += gridDim.x * blockDim.x) {
-    sc a = reduce_limb_sums(key_acc + (size_t)j * PL);
-    store_coeff(scal, 1 + n + j, n + m + 1 + j, a, few);
+  const bool per_sig = per_sig_host || flags[FLAG_OVF];
+  const uint32_t m = per_sig ? 0u : (uint32_t)flags[FLAG_NKEYS];
+  for (uint32_t j = j0; j < m; j += gridDim.x * blockDim.x) store_scalar(scal, 1 + n + j, reduce_limb_sums(key_acc + (size_t)j * PL));
+  if (j0 == 0) store_scalar(scal, 0, sc_sub(sc_zero(), reduce_limb_sums(u_acc)));
+}
+
+// Range mode (grouped fallback): listed MSM terms (point, range, scalar). Pairs q = g m + j
+// (grouped keys) -> (n+1+j, g, sum z k of key j in range g); then one B term per range g ->
+// (0, g, -sum z s of range g). Absent pairs have scalar 0 and produce no digits.
+__global__ void __launch_bounds__(256) k_range_terms(uint32_t n, uint32_t nranges, uint32_t m,
+                                                     const unsigned long long* __restrict__ key_acc,
+                                                     const unsigned long long* __restrict__ u_acc,
+                                                     uint32_t* __restrict__ xpt, uint32_t* __restrict__ xrg,
+                                                     uint32_t* __restrict__ xscal) {
+  const uint32_t npair = nranges * m;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < npair + nranges; q += gridDim.x * blockDim.x) {
+    if (q < npair) {
+      xpt[q] = 1 + n + q % m;
+      xrg[q] = q / m;
+      store_scalar(xscal, q, reduce_limb_sums(key_acc + (size_t)q * PL));
+    } else {
+      const uint32_t g = q - npair;
+      xpt[q] = 0;
+      xrg[q] = g;
+      store_scalar(xscal, q, sc_sub(sc_zero(), reduce_limb_sums(u_acc + (size_t)g * PL)));
+    }
   }
-  const uint32_t j = j0;
-  if (j == 0) {
-    sc u = reduce_limb_sums(u_acc);
-    store_coeff(scal, 0, n + 2 * m + 1, sc_sub(sc_zero(), u), few);
-  }
+}
+
+// Range mode: rbad[g] = 1 iff range g holds an item whose R or s failed, or whose key failed to
+// decode (such ranges are verified item by item whatever their partial point).
+__global__ void __launch_bounds__(256) k_range_prebad(uint32_t n, uint32_t rsize, const uint8_t* __restrict__ itembad,
+                                                      const uint8_t* __restrict__ keybad,
+                                                      const uint32_t* __restrict__ key_index, int per_sig,
+                                                      uint8_t* __restrict__ rbad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (itembad[i] || keybad[per_sig ? i : key_index[i]]) rbad[i / rsize] = 1;
 }
 
 __global__ void k_init_basepoint(uint32_t* pts) {
@@ -427,43 +427,59 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
   if (n)
     hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, SHA_THREADS)), dim3(SHA_THREADS), 0, st, n, vk, sig, msg, off, k);
 }
-void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, uint32_t* pts, int* flags) {
-  if (n) hipLaunchKernelGGL(k_decompress, dim3(cdiv(n, 256)), dim3(256), 0, st, n, sig, pts, flags);
-}
-void launch_key_points(hipStream_t st, uint32_t n, const uint8_t* vk, const uint32_t* key_rep, uint32_t* pts,
-                       const uint32_t* bshift, int* flags, const KeyCacheView& kc) {
-  if (!n) return;
-  // grids cover the largest possible m (n distinct keys; few-key mode: m <= n / 16); m is read
-  // on the device and surplus blocks exit at once
-  // one lane per possible key (a distinct-key batch decodes n keys at full occupancy, VALU-bound
-  // like k_decompress); lanes beyond the device-side m exit at once
-  hipLaunchKernelGGL(k_key_points, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, key_rep, pts, flags, kc);
-  if (n >= FEW_KEY_MIN_N)
-    hipLaunchKernelGGL(k_key_shift, dim3(grid_cap(cdiv(4ull * (n / FEW_KEY_RATIO) + NIELS_WORDS, 64), 1024)),
-                       dim3(64), 0, st, n, vk, key_rep, pts, bshift, flags, kc);
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
+                       bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
+                       const KeyCacheView& kc) {
+  // lanes [0, n) decode R_i, lanes [n, 2n) cover the largest possible key count (m <= n)
+  if (n)
+    hipLaunchKernelGGL(k_decompress, dim3(cdiv(2ull * n, 256)), dim3(256), 0, st, n, sig, vk, key_rep,
+                       per_sig ? 1 : 0, pts, itembad, keybad, flags, kc);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
-                 uint32_t salt, uint32_t* slot_key, uint32_t* key_slot_of_sig, uint32_t* key_rep,
-                 uint32_t* key_index, uint32_t* pts, unsigned long long* key_acc, int* flags) {
+                 const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
+                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags) {
   if (!n) return;
-  hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt,
+  hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt[0], salt[1],
+                     force_overflow ? 0u : KEY_PROBE_CAP,
                      slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
-                     key_index);
+                     key_index, flags);
 }
 void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags) {
   (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags + FLAG_NKEYS), (int)n, 1, st);
 }
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
-                 unsigned long long* key_acc, unsigned long long* u_acc, int* flags, bool per_sig) {
+                 unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
+                 bool per_sig) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
-                       key_index, scal, key_acc, u_acc, flags, per_sig ? 1 : 0);
+                       key_index, scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u);
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
                      u_acc, scal, flags, per_sig ? 1 : 0);
+}
+void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nranges, uint32_t m, bool per_sig,
+                       const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],
+                       uint64_t zbase, const uint32_t* key_index, uint32_t* scal, unsigned long long* key_acc,
+                       unsigned long long* u_acc, int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal) {
+  seed8 s;
+  for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
+  const uint32_t mm = per_sig ? 0u : m;
+  (void)hipMemsetAsync(key_acc, 0, (size_t)nranges * mm * PL * sizeof(unsigned long long), st);
+  (void)hipMemsetAsync(u_acc, 0, (size_t)nranges * PL * sizeof(unsigned long long), st);
+  if (n)
+    hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
+                       key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm);
+  hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
+                     n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
+}
+void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* keybad,
+                         const uint32_t* key_index, bool per_sig, uint8_t* rbad) {
+  if (n)
+    hipLaunchKernelGGL(k_range_prebad, dim3(cdiv(n, 256)), dim3(256), 0, st, n, rsize, itembad, keybad, key_index,
+                       per_sig ? 1 : 0, rbad);
 }
 // Key-indexed host submissions (edc_batch_submit_indexed): item i's raw key bytes from the key
 // cache, vk_out[i] = keys[reg[key_idx[i]]] (indices were range-checked on the host), so the
@@ -482,6 +498,28 @@ void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, con
                         const uint32_t* keys, uint8_t* vk_out) {
   if (n) hipLaunchKernelGGL(k_expand_keys, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_idx, reg, keys,
                             reinterpret_cast<uint32_t*>(vk_out));
+}
+// grouped fallback: the items to verify one by one, gathered into contiguous staging buffers
+__global__ void __launch_bounds__(256) k_gather_items(uint32_t c, const uint32_t* __restrict__ idx,
+                                                      const uint8_t* __restrict__ vk, const uint8_t* __restrict__ sig,
+                                                      const uint32_t* __restrict__ k, uint8_t* __restrict__ out_vk,
+                                                      uint8_t* __restrict__ out_sig, uint32_t* __restrict__ out_k) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  const size_t i = idx[j];
+  const uint4* a = reinterpret_cast<const uint4*>(vk + i * 32);
+  uint4* da = reinterpret_cast<uint4*>(out_vk + (size_t)j * 32);
+  da[0] = a[0]; da[1] = a[1];
+  const uint4* b = reinterpret_cast<const uint4*>(sig + i * 64);
+  uint4* db = reinterpret_cast<uint4*>(out_sig + (size_t)j * 64);
+  db[0] = b[0]; db[1] = b[1]; db[2] = b[2]; db[3] = b[3];
+  const uint4* q = reinterpret_cast<const uint4*>(k + i * 8);
+  uint4* dq = reinterpret_cast<uint4*>(out_k + (size_t)j * 8);
+  dq[0] = q[0]; dq[1] = q[1];
+}
+void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const uint8_t* vk, const uint8_t* sig,
+                         const uint32_t* k, uint8_t* out_vk, uint8_t* out_sig, uint32_t* out_k) {
+  if (c) hipLaunchKernelGGL(k_gather_items, dim3(cdiv(c, 256)), dim3(256), 0, st, c, idx, vk, sig, k, out_vk, out_sig, out_k);
 }
 void launch_init_basepoint(hipStream_t st, uint32_t* pts) {
   hipLaunchKernelGGL(k_init_basepoint, dim3(1), dim3(64), 0, st, pts);

@@ -17,19 +17,15 @@ __device__ __forceinline__ ge_niels to_niels(const ge_p3& P) {  // x = X/Z, y = 
   return ge_to_niels_affine(a);
 }
 
-// context constants as affine Niels: [i]B for i = 1..8 (entries 0..7) and [2^128]B (entry
-// BTAB_BSHIFT, the few-key MSM's shifted basepoint)
+// context constants as affine Niels: [i]B for i = 1..8 (entries 0..7)
 __global__ void k_init_btable(uint32_t* btab) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ge_p3 B = ge_basepoint();
   ge_p3 acc = B;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < BTAB_ENTRIES; ++i) {
     st_niels(btab, i, to_niels(acc));
     acc = ge_add(acc, B);
   }
-  acc = B;
-  for (int k = 0; k < 128; ++k) acc = ge_dbl(acc);
-  st_niels(btab, BTAB_BSHIFT, to_niels(acc));
 }
 
 // signed radix-16 digits of a scalar < 2^255, 64 digits in [-7, 8]

@@ -12,7 +12,10 @@
  *  - Items are in QUEUE order. vk: n*32 bytes, sig: n*64 bytes (R || s), messages are one
  *    arena `msg` with n+1 offsets (message i = msg[msg_off[i] .. msg_off[i+1])).
  *  - z_i = u128::from_le_bytes(ChaCha20Rng::from_seed(z_seed) keystream[16(z_base+i) ..]),
- *    i.e. gen_u128 (reference src/batch.rs:64-68) drawn in queue order.
+ *    i.e. gen_u128 (reference src/batch.rs:64-68) drawn in queue order. Batch verification is
+ *    sound only when z is unpredictable to the signers: z_seed must come from a CSPRNG, fresh for
+ *    every verification (the reference takes `impl RngCore + CryptoRng`). Fixed seeds are for
+ *    reproducible tests and benchmarks only.
  *  - Return codes: EDC_OK / EDC_INVALID_SIGNATURE / EDC_MALFORMED_PUBLIC_KEY mirror
  *    ed25519_consensus::Error (reference src/error.rs:7-20); negative = runtime failure
  *    (never mapped to Ok by callers).
@@ -141,15 +144,36 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
 
 /*
  * Grouped fallback after a failed batch (the caller-driven Item::verify_single loop of
- * reference tests/batch.rs:37-43, src/batch.rs:104-107, done by bisection): the batch equation is
- * linear, so a range's check point minus its left half's is its right half's; ranges whose
- * [8]*check is the identity are valid (ZIP215: batch == single), failing ranges are halved
- * until <= leaf items, which are verified one by one. verdicts (host, n bytes) equal
+ * reference tests/batch.rs:37-43, src/batch.rs:104-107). The batch equation is linear, so it
+ * restricts to any subset of the items: ONE range-tagged MSM pass evaluates it over ~256
+ * contiguous ranges (same z, same k, the decoded points of the batch prefix); ranges whose
+ * [8]*check is not the identity, or that hold an item with an undecodable R / key or a
+ * non-canonical s, are verified item by item. verdicts (host, n bytes) receive
  * Item::verify_single's code for every item. Returns the number of invalid items, or <0.
+ * `leaf` is ignored (kept for ABI compatibility): range sizes are chosen by the library.
+ *
+ * Soundness: an item of a passing range is reported valid because its range's batch equation
+ * holds, exactly as Verifier::verify accepts a batch (ZIP215: batch == single). Like the
+ * reference's batch verification this is probabilistic: it relies on z being unpredictable to
+ * whoever made the signatures. z_seed MUST be fresh and secret for every call (e.g. 32 bytes
+ * of OS randomness); a known or reused seed lets crafted invalid signatures cancel inside a
+ * range and be reported valid.
  */
 int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                             const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
                             size_t leaf, uint8_t* verdicts);
+
+/*
+ * Verifier::verify(rng) and, if it fails, the per-item fallback in one call (the flow of
+ * reference tests/batch.rs:18-44): the batch runs once; on failure the grouped fallback above
+ * reuses that batch's k, points and grouping instead of recomputing them. Returns EDC_OK
+ * (verdicts all 0) or EDC_INVALID_SIGNATURE with verdicts[i] = Item::verify_single's code and
+ * *n_invalid (nullable) their count; <0 on runtime failure. check8 (nullable) as
+ * edc_batch_verify. Same z_seed requirement as edc_find_invalid_device.
+ */
+int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                     const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                                     uint8_t* verdicts, int* n_invalid, uint8_t check8[32]);
 
 /*
  * batch::Item::verify_single (reference src/batch.rs:104-107): as edc_verify_each but with the
@@ -217,9 +241,19 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
  * repeat. mode 0 (default, auto): group, unless the last grouped batch on this context had more
  * distinct keys than half its signatures, in which case the next batches (regrouping every 8th)
  * keep one A_i term per signature with coefficient z_i k_i. mode 1: always group. mode 2: never.
+ * mode 3 (tests): group, but with a zero probe budget, so every batch takes the on-device
+ * overflow path that an adversarial key set would trigger (grouping abandoned mid-batch, one key
+ * term per signature). Grouping hashes the raw key bytes under a per-context secret from OS
+ * randomness and caps its probes, so chosen keys cannot make it quadratic.
  * Every mode gives the same group element, hence identical verdicts and [8]*check.
  */
 int edc_set_key_grouping(edc_ctx* ctx, int mode);
+
+/*
+ * Pippenger window width for this context's batches: 0 (default) picks it from the batch size;
+ * 8..16 forces it (tuning / measurement). Results never depend on it.
+ */
+int edc_set_window_bits(edc_ctx* ctx, int bits);
 
 /*
  * Pre-allocate the workspaces of every in-flight slot for batches of up to n items (otherwise

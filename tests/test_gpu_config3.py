@@ -57,6 +57,12 @@ def test_config3_corpus_and_bad_sig_in_2_20_votes(engine):
     got_group = {i: raw[i] for i in expect}
     assert got_group == expect and raw.count(0) == n - 1
 
+    # batch + fallback in one call (the failed batch's k, points and grouping reused)
+    v2 = ctypes.create_string_buffer(n)
+    cnt = ctypes.c_int(-1)
+    assert lib.edc_batch_verify_fallback_device(engine.ctx, n, *args, zseed, v2, ctypes.byref(cnt), None) == 1
+    assert cnt.value == 1 and {i: v2.raw[i] for i in expect} == expect and v2.raw.count(0) == n - 1
+
     # the valid remainder, corpus included, is one valid batch
     keep = torch.ones(n, dtype=torch.bool, device=dev)
     keep[list(expect)] = False

@@ -72,6 +72,12 @@ def test_corpus_mixed_batch_grouped_fallback(engine, n, keys):
     assert each == expect
     assert got == expect
     assert nbad == 4
+    # batch + fallback in one call (reuses the failed batch's k, points and grouping)
+    v2 = ctypes.create_string_buffer(n)
+    cnt = ctypes.c_int(-1)
+    rc = lib.edc_batch_verify_fallback_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
+                                              d_off.data_ptr(), zseed, v2, ctypes.byref(cnt), None)
+    assert rc == 1 and cnt.value == 4 and list(v2.raw) == expect
     # and the valid remainder (bad items removed) verifies as one batch
     keep = [i for i in range(n) if expect[i] == 0]
     code, c8 = engine.batch_verify([vks[i] for i in keep], [sigs[i] for i in keep], [msgs[i] for i in keep],

@@ -4,7 +4,9 @@ signature made over another message mixed in at seeded positions (bench.make_c4_
 device-resident:
   batch      the failing batch verification (edc_batch_verify_device)
   per_sig    the reference's fallback, Item::verify_single on every item (edc_verify_each_device)
-  grouped    the grouped fallback (edc_find_invalid_device)
+  grouped    the grouped fallback (edc_find_invalid_device: batch prefix + range MSM + leaves)
+  fused      batch + fallback in one call (edc_batch_verify_fallback_device), the fallback part
+             reusing the failed batch's k, points and grouping
 and checks that both fallbacks return exactly the expected per-item codes (the bad item
 InvalidSignature, every corpus case and every other vote Ok). Prints one JSON line.
   python tools/fallback_bench.py [--n 1048576] [--leaf 65536] [--keycache]"""
@@ -71,8 +73,17 @@ def main():
         raw = verdicts.raw
         flagged_group = {i: raw[i] for i in range(n) if raw[i]}
         assert flagged_each == flagged_group == expect, (flagged_each, flagged_group, expect)
+        cnt = ctypes.c_int(0)
+        rc, t_fused = timed(lambda: lib.edc_batch_verify_fallback_device(eng.ctx, n, *a, zseed, verdicts,
+                                                                         ctypes.byref(cnt), None))
+        assert rc == 1 and cnt.value == len(expect)
+        raw = verdicts.raw
+        assert {i: raw[i] for i in range(n) if raw[i]} == expect
         return {"batch_ms": round(t_batch, 3), "per_sig_fallback_ms": round(t_each, 3),
                 "grouped_fallback_ms": round(t_group, 3), "grouped_over_batch": round(t_group / t_batch, 3),
+                "batch_plus_fallback_ms": round(t_fused, 3),
+                "fallback_after_batch_ms": round(t_fused - t_batch, 3),
+                "fallback_after_batch_over_batch": round((t_fused - t_batch) / t_batch, 3),
                 "per_sig_sigs_per_s": round(n / t_each * 1e3, 1)}
 
     out = {"workload": "configs[3]: 2^20 votes / 150 validators / 120-B msgs + 196 ZIP215 corpus cases + 1 bad sig",
