@@ -43,7 +43,7 @@ ABI_SYMBOLS = [
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
     "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
-    "edc_set_window_bits",
+    "edc_set_window_bits", "edc_set_fallback_shape",
 ]
 
 
@@ -117,6 +117,7 @@ def load_library(path=None):
         lib.edc_batch_verify_fallback_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_vp,
                                                          ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_set_window_bits.argtypes = [c_vp, ctypes.c_int]
+        lib.edc_set_fallback_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]

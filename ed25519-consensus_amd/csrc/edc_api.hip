@@ -27,6 +27,7 @@ hipError_t dalloc(T** p, size_t count) {
 }
 
 constexpr int kSlots = 4;  // batches that can be in flight per context
+constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
 }  // namespace
 
@@ -100,6 +101,8 @@ struct edc_ctx {
   uint8_t* fb_rv = nullptr;      // per-range verdict | pre-bad flag
   uint32_t* fb_idx = nullptr;    // items verified one by one
   size_t fb_cap_idx = 0;
+  uint32_t fb_ranges = 32;      // target range count of the grouped fallback
+  int fb_bits = 10;             // its window width
   // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
   uint32_t *kc_table = nullptr, *kc_keys = nullptr, *kc_comb = nullptr;
   uint8_t* kc_ok = nullptr;
@@ -876,8 +879,11 @@ static int verify_listed(edc_ctx* ctx, Slot& s, const std::vector<uint32_t>& idx
   hipStream_t st = s.st;
   CK(hipMemcpyAsync(ctx->fb_idx, idx.data(), c * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   launch_gather_items(st, (uint32_t)c, ctx->fb_idx, d_vk, d_sig, s.k, ctx->vk, ctx->sig, ctx->kbuf);
-  launch_verify_single(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts, ctx->kc(),
-                       ctx->bcomb);
+  if (c <= kQuadVerifyMax)   // latency-bound: one quad of lanes per item
+    launch_verify_quad(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts, ctx->kc(), ctx->bcomb);
+  else
+    launch_verify_single(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts,
+                         ctx->kc(), ctx->bcomb);
   CK(hipGetLastError());
   std::vector<uint8_t> v(c);
   CK(hipMemcpyAsync(v.data(), ctx->verdicts, c, hipMemcpyDeviceToHost, st));
@@ -900,7 +906,10 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
                            bool per_sig, uint32_t m, uint8_t* verdicts) {
   memset(verdicts, 0, n);
   if (!n) return 0;
-  const size_t target = (n + 255) / 256;
+  // ~FB_RANGES ranges: each range-window bin then holds enough digits to amortize its fixed
+  // 256-bucket reduction, and a failing range costs no more than a small one in the per-item pass
+  // (that pass is latency-bound: one lane per item)
+  const size_t target = (n + ctx->fb_ranges - 1) / ctx->fb_ranges;
   const size_t rsize = (target + COEF_CHUNK - 1) / COEF_CHUNK * COEF_CHUNK;
   const uint32_t G = (uint32_t)((n + rsize - 1) / rsize);
   if (!per_sig && (size_t)G * m > s.cap_n) {
@@ -911,7 +920,7 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
     CK(hipStreamSynchronize(s.st));
     per_sig = true;
   }
-  const MsmPlan P = make_plan(9, 9, G);
+  const MsmPlan P = make_plan(ctx->fb_bits, ctx->fb_bits, G);
   const uint32_t mm = per_sig ? 0u : m;
   const size_t nx = (size_t)G * (mm + 1);
   const uint32_t npoint = (uint32_t)(per_sig ? 2 * n : n);
@@ -1159,6 +1168,13 @@ int edc_set_key_grouping(edc_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 3) return EDC_ERR_ARG;
   ctx->key_grouping = mode;
   ctx->ungrouped_run = 0;
+  return 0;
+}
+
+int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits) {
+  if (!ctx || ranges < 1 || ranges > 1024 || bits < 8 || bits > 13) return EDC_ERR_ARG;
+  ctx->fb_ranges = (uint32_t)ranges;
+  ctx->fb_bits = bits;
   return 0;
 }
 

@@ -53,6 +53,9 @@ void launch_init_btable(hipStream_t st, uint32_t* btab);
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                           const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict,
                           const KeyCacheView& kc, const uint32_t* bcomb);
+// latency form for short item lists (one quad of lanes per item)
+void launch_verify_quad(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig, const uint32_t* k,
+                        const uint32_t* btab, uint8_t* verdict, const KeyCacheView& kc, const uint32_t* bcomb);
 // key cache (edc_single.hip): decode m registered keys -> ext + ok, comb tables of m points
 void launch_kc_decode(hipStream_t st, uint32_t m, const uint32_t* keys, uint32_t* ext, uint8_t* ok);
 void launch_kc_basepoint(hipStream_t st, uint32_t* ext);

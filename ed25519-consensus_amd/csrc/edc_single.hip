@@ -7,6 +7,7 @@
 //   k_decode         CompressedEdwardsY::decompress for the API (canonical x||y + verdict)
 #include "edc_common.h"
 #include "edc_launch.h"
+#include "ge_quad.h"
 
 namespace edc {
 
@@ -199,6 +200,76 @@ __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_single(uint32_t n, con
   verdict[i] = ge_is_identity(ge_mul_by_cofactor(d)) ? 0 : 1;
 }
 
+// Latency form of k_verify_single for small item lists (the grouped fallback's failing ranges):
+// one QUAD of lanes per item (ge_quad.h), so every point operation of the 252-doubling chain is
+// two rounds of one field multiplication per lane instead of eight serial ones. A and R are
+// decoded at once on different lanes of the quad; the table of [1..8](-A) and the parked R live
+// in LDS. Same verdict codes as k_verify_single; items with a cached key are left to
+// k_verify_comb.
+constexpr int VQ_ITEMS = 16;                       // items per 64-lane workgroup
+__global__ void __launch_bounds__(64) k_verify_quad(uint32_t n, const uint8_t* __restrict__ vk,
+                                                    const uint8_t* __restrict__ sig,
+                                                    const uint32_t* __restrict__ kscal,
+                                                    const uint32_t* __restrict__ btab,
+                                                    uint8_t* __restrict__ verdict, KeyCacheView kcache) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[VQ_ITEMS][9 * EXT_WORDS];
+  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 2;
+  const int q = (int)(threadIdx.x & 3);
+  uint32_t* tab = lds[threadIdx.x >> 2];
+  if (i >= n) return;                              // whole quads leave together
+  uint32_t aw[8], rw[8], sw[8];
+  ld_words8(vk + (size_t)i * 32, aw);
+  if (kc_lookup(kcache, aw) >= 0) return;          // done by k_verify_comb
+  ld_words8(sig + (size_t)i * 64, rw);
+  ld_words8(sig + (size_t)i * 64 + 32, sw);
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = q == 1 ? rw[j] : aw[j];
+  ge_p3 D;
+  const bool ok = ge_decompress(w, D);             // lane 1: R, the others: A
+  const uint32_t okA = quad_bcast<0>(ok ? 1u : 0u), okR = quad_bcast<1>(ok ? 1u : 0u);
+  if (!okA) { if (q == 0) verdict[i] = 2; return; }          // try_from: MalformedPublicKey
+  if (!sc_is_canonical(sw)) { if (q == 0) verdict[i] = 1; return; }   // s checked before R
+  if (!okR) { if (q == 0) verdict[i] = 1; return; }
+  const ge_p3 R = quad_bcast_point<1>(D);
+  if (q == 0) st_ext(tab + 8 * EXT_WORDS, R);      // parked: not live across the loop
+  const ge_p3 nA = ge_neg(quad_bcast_point<0>(D));
+  const ge_cached c1 = ge_to_cached(nA);
+  ge_p3 acc = nA;
+  if (q == 0) st_cached(tab, c1);
+  for (int d = 1; d < 8; ++d) {
+    acc = quad_add_cached(acc, c1);
+    const ge_cached cd = ge_to_cached(acc);
+    if (q == 0) st_cached(tab + d * EXT_WORDS, cd);
+  }
+  uint32_t k[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  const uint64_t kc = radix16_carries(k), sc = radix16_carries(sw);
+  acc = ge_identity();
+  for (int j = 63; j >= 0; --j) {                  // R' = [k](-A) + [s]B
+    if (j != 63) {
+      acc = quad_dbl(acc);
+      acc = quad_dbl(acc);
+      acc = quad_dbl(acc);
+      acc = quad_dbl(acc);
+    }
+    const int a = radix16_digit(k, kc, j);
+    const int ai = a < 0 ? -a : a;
+    ge_cached qa = ai ? ld_cached(tab + (ai - 1) * EXT_WORDS) : cached_identity();
+    if (a < 0) qa = ge_cached_neg(qa);
+    acc = quad_add_cached(acc, qa);
+    const int b = radix16_digit(sw, sc, j);
+    const int bi = b < 0 ? -b : b;
+    ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
+    if (b < 0) nb = ge_niels_neg(nb);
+    acc = quad_madd(acc, nb);
+  }
+  ge_p3 d = quad_add(ld_ext(tab + 8 * EXT_WORDS), ge_neg(acc));
+  d = quad_dbl(quad_dbl(quad_dbl(d)));
+  if (q == 0) verdict[i] = ge_is_identity(d) ? 0 : 1;
+}
+
 // [x]B, x < 2^256
 __device__ ge_p3 base_mul(const uint32_t x[8], const uint32_t* btab) {
   int8_t d[64];
@@ -360,6 +431,14 @@ void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const u
                        bcomb);
   hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, btab,
                      vtab, verdict, kc);
+}
+void launch_verify_quad(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig, const uint32_t* k,
+                        const uint32_t* btab, uint8_t* verdict, const KeyCacheView& kc, const uint32_t* bcomb) {
+  if (!n) return;
+  if (kc.table)
+    hipLaunchKernelGGL(k_verify_comb, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, verdict, kc,
+                       bcomb);
+  hipLaunchKernelGGL(k_verify_quad, dim3(cdiv(4ull * n, 64)), dim3(64), 0, st, n, vk, sig, k, btab, verdict, kc);
 }
 void launch_kc_decode(hipStream_t st, uint32_t m, const uint32_t* keys, uint32_t* ext, uint8_t* ok) {
   if (m) hipLaunchKernelGGL(k_kc_decode, dim3(cdiv(m, 256)), dim3(256), 0, st, m, keys, ext, ok);

@@ -78,6 +78,38 @@ __device__ __forceinline__ ge_p3 quad_add_cached(const ge_p3& P, const ge_cached
   return r;
 }
 
+// P + Q, Q affine Niels (Z2 = 1): three products in the first round (lane 3 repeats lane 2's)
+__device__ __forceinline__ ge_p3 quad_madd(const ge_p3& P, const ge_niels& Q) {
+  const int q = quad_lane();
+  fe a = quad_pick(q, fe_sub(P.Y, P.X), fe_add(P.Y, P.X), P.T, P.T);
+  fe b = quad_pick(q, Q.ymx, Q.ypx, Q.xy2d, Q.xy2d);
+  fe m = fe_mul(a, b);
+  fe A, B, C, C2;
+  quad_gather(m, A, B, C, C2);
+  fe D = fe_add_c(P.Z, P.Z);
+  fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  fe a2 = quad_pick(q, E, G, F, E);
+  fe b2 = quad_pick(q, F, H, G, H);
+  fe m2 = fe_mul(a2, b2);
+  ge_p3 r;
+  quad_gather(m2, r.X, r.Y, r.Z, r.T);
+  return r;
+}
+
+// the point held by lane J of each quad, on every lane of the quad
+template <int J>
+__device__ __forceinline__ ge_p3 quad_bcast_point(const ge_p3& P) {
+  ge_p3 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    r.X.v[i] = quad_bcast<J>(P.X.v[i]);
+    r.Y.v[i] = quad_bcast<J>(P.Y.v[i]);
+    r.Z.v[i] = quad_bcast<J>(P.Z.v[i]);
+    r.T.v[i] = quad_bcast<J>(P.T.v[i]);
+  }
+  return r;
+}
+
 // P + Q, both extended (one extra multiplication round for T2 * 2d)
 __device__ __forceinline__ ge_p3 quad_add(const ge_p3& P, const ge_p3& Q) {
   ge_cached c;

@@ -256,6 +256,13 @@ int edc_set_key_grouping(edc_ctx* ctx, int mode);
 int edc_set_window_bits(edc_ctx* ctx, int bits);
 
 /*
+ * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous
+ * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). Results never depend
+ * on it.
+ */
+int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits);
+
+/*
  * Pre-allocate the workspaces of every in-flight slot for batches of up to n items (otherwise
  * they grow on first use). Not a reference API: a setup call for streaming callers.
  */

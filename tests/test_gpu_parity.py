@@ -324,3 +324,44 @@ def test_host_submit_indexed_equals_fixture(engine, name):
                                         bytes.fromhex(b["z_seed"]))
     finally:
         engine.keycache_clear()
+
+
+def _dev_batch(torch, it, dev):
+    vk = torch.tensor(list(b"".join(v for v, _, _ in it)) or [0], dtype=torch.uint8, device=dev)
+    sg = torch.tensor(list(b"".join(s for _, s, _ in it)) or [0], dtype=torch.uint8, device=dev)
+    mg = torch.tensor(list(b"".join(m for _, _, m in it)) or [0], dtype=torch.uint8, device=dev)
+    offs = [0]
+    for _, _, m in it:
+        offs.append(offs[-1] + len(m))
+    return vk, sg, mg, torch.tensor(offs, dtype=torch.int64, device=dev)
+
+
+@pytest.mark.parametrize("b", golden("batches.json")["batches"], ids=lambda b: b["name"])
+@pytest.mark.parametrize("shape", [(32, 10), (1024, 8)])
+def test_batch_then_fallback_fixture(engine, b, shape):
+    """edc_batch_verify_fallback_device (batch, then the one-pass grouped fallback and the quad
+    per-item kernel on the failing ranges) returns the fixture's batch code, [8]*check and, for a
+    failed batch, exactly Item::verify_single's code for every item."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+    it = _items(b)
+    n = len(it)
+    dev = torch.device("cuda:0")
+    vk, sg, mg, off = _dev_batch(torch, it, dev)
+    torch.cuda.synchronize()
+    lib = engine.lib
+    assert lib.edc_set_fallback_shape(engine.ctx, *shape) == 0
+    try:
+        v = ctypes.create_string_buffer(max(n, 1))
+        cnt = ctypes.c_int(-1)
+        c8 = ctypes.create_string_buffer(32)
+        rc = lib.edc_batch_verify_fallback_device(engine.ctx, n, vk.data_ptr(), sg.data_ptr(), mg.data_ptr(),
+                                                  off.data_ptr(), bytes.fromhex(b["z_seed"]), v, ctypes.byref(cnt), c8)
+    finally:
+        lib.edc_set_fallback_shape(engine.ctx, 32, 10)
+    assert rc == b["expect_code"]
+    if b["expect_check8"] is not None:
+        assert c8.raw.hex() == b["expect_check8"]
+    exp = b["expect_single"] if rc else [0] * n
+    assert list(v.raw[:n]) == exp
+    assert cnt.value == (sum(1 for e in exp if e) if rc else 0)

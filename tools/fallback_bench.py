@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--leaf", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--keycache", action="store_true", help="also time with the validator keys in the key cache")
+    ap.add_argument("--shapes", default="", help="sweep fallback shapes 'ranges:bits,...' (edc_set_fallback_shape)")
     args = ap.parse_args()
     import torch
     import bench
@@ -90,6 +91,12 @@ def main():
            "n": n, "validators": args.keys, "corpus_cases": len(cpos), "expected_invalid": expect,
            "leaf": args.leaf, "timing": "best of %d, device-resident, synchronous" % args.reps}
     out.update(run_all())
+    for sh in [x for x in args.shapes.split(",") if x]:
+        r, b = (int(v) for v in sh.split(":"))
+        eng._check(lib.edc_set_fallback_shape(eng.ctx, r, b))
+        out.setdefault("shapes", {})[sh] = run_all()
+    if args.shapes:
+        eng._check(lib.edc_set_fallback_shape(eng.ctx, 32, 10))
     if args.keycache and args.keys:
         keys = bytes(vk[:32 * args.keys].cpu().tolist())
         t0 = time.perf_counter()
