@@ -25,6 +25,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 ALG_MAD_M, ALG_MAD_S = 64, 40
 DECOMP_S, DECOMP_M = 255, 22                     # ZIP215 decode + Niels conversion, per point
 ALG_MAD_DECOMP = DECOMP_S * ALG_MAD_S + DECOMP_M * ALG_MAD_M
+# whole-path algorithmic work per signature, frozen by SURVEY.md 8(d): decompression 255 S + 20 M
+# = 11,480 per point, MSM 7 M = 448 per point-window at c = 16 (R terms 8 windows, A terms 16)
+ALG_MAD_PER_SIG_REPEATED = 11480 + 8 * 448            # configs[2]/[3]: repeated validator keys, 15,064
+ALG_MAD_PER_SIG_DISTINCT = 2 * 11480 + 24 * 448       # configs[1]/[4]: distinct keys, 33,712
 # peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, v_mad_u64_u32 at half lane rate (measured
 # 35.0 T/s sustained by tools/microbench/valu_rates.hip, profiles/r01_valu_rates.txt)
 PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12
@@ -161,6 +165,10 @@ def main():
     ap.add_argument("--inflight", type=int, default=4, help="batches in flight per GPU (submit/wait pipelining)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank verifies --n signatures of one global batch; strong: the ranks split "
+                         "one batch of --n signatures (n/G each)")
+    ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -191,7 +199,7 @@ def main():
     from importlib import import_module
     sharded = import_module("ed25519_consensus_amd.sharded")
 
-    n = args.n
+    n = args.n // world if args.scaling == "strong" else args.n
     base = rank * n
     t_gen = time.perf_counter()
     vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
@@ -239,7 +247,8 @@ def main():
     if args.keycache and args.keys > 0:           # a node's known validator set, registered once
         kb = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
         eng.keycache_load([kb[32 * i:32 * i + 32] for i in range(len(kb) // 32)])
-    eng._check(lib.edc_reserve(eng.ctx, n))        # both in-flight slots' workspaces, before any step
+    eng._check(lib.edc_set_window_bits(eng.ctx, args.window_bits))
+    eng._check(lib.edc_reserve(eng.ctx, n))        # every in-flight slot's workspace, before any step
     run_steps(args.warmup)
     if dist:
         dist.barrier()
@@ -296,7 +305,7 @@ def main():
     phases = {names[i]: round(acc[i], 4) for i in range(7)}
 
     if rank == 0:
-        total = n * world * args.steps
+        total = n * world * args.steps          # strong scaling: n * world == --n
         value = total / elapsed
         ms_per_step = elapsed / args.steps * 1e3
         dom_ms = phases["decompress_R"]
@@ -327,6 +336,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
             cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
+        alg_sig = ALG_MAD_PER_SIG_REPEATED if args.keys > 0 else ALG_MAD_PER_SIG_DISTINCT
         line = {
             "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
             "value": round(value, 1),
@@ -336,7 +346,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u32/u64 integer (GF(2^255-19), radix 2^29 limbs)",
             "data": "synthetic (ChaCha20-seeded keys/messages, signed on GPU)",
@@ -349,6 +359,12 @@ def main():
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
                          "traffic": traffic, "pmc_valu": valu,
                          "alg_mad_per_unit": ALG_MAD_DECOMP, "units_per_launch": units,
+                         "pipeline": {"alg_mad_per_sig": alg_sig,
+                                      "achieved": round(value / world * alg_sig / 1e12, 3),
+                                      "peak": round(PEAK_TMAD, 2), "unit": "T v_mad_u64_u32/s per GPU",
+                                      "frac": round(value / world * alg_sig / 1e12 / PEAK_TMAD, 4),
+                                      "basis": "whole hot path: sigs/s per GPU x SURVEY.md 8(d) ALG_MAD_PER_SIG "
+                                               "(decompression + MSM additions) / peak"},
                          "avg_launch_ms": dom_ms,
                          "pipelined": {"avg_launch_ms": round(pipe_dec_ms, 4),
                                        "achieved": round(units * ALG_MAD_DECOMP / (pipe_dec_ms * 1e-3) / 1e12, 3),

@@ -43,7 +43,8 @@ ABI_SYMBOLS = [
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
     "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
-    "edc_set_window_bits", "edc_set_fallback_shape",
+    "edc_set_window_bits", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
+    "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
 ]
 
 
@@ -118,6 +119,17 @@ def load_library(path=None):
                                                          ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_set_window_bits.argtypes = [c_vp, ctypes.c_int]
         lib.edc_set_fallback_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
+        lib.edc_create_multi.restype = c_vp
+        lib.edc_create_multi.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        lib.edc_destroy_multi.argtypes = [c_vp]
+        lib.edc_multi_size.argtypes = [c_vp]
+        lib.edc_multi_context.restype = c_vp
+        lib.edc_multi_context.argtypes = [c_vp, ctypes.c_int]
+        lib.edc_multi_last_error.restype = ctypes.c_char_p
+        lib.edc_multi_last_error.argtypes = [c_vp]
+        lib.edc_multi_batch_verify.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp]
+        lib.edc_multi_batch_verify_fallback.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp,
+                                                        ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]
@@ -337,6 +349,61 @@ class Engine:
             rc = self._check(self.lib.edc_combine_partials(self.ctx, len(partials), b"".join(partials) or b"\0",
                                                            1 if bad_any else 0, check8))
         return rc, (check8.raw if check8 is not None else None)
+
+
+class MultiEngine:
+    """Several GPUs in one process (include/edc.h edc_create_multi): each batch is split into
+    contiguous shards, one per listed device; partial points are combined on the first device.
+    A device may be listed several times (several contexts on one GPU)."""
+
+    def __init__(self, devices):
+        self.lib = load_library()
+        if self.lib.edc_device_count() <= 0:
+            raise EngineError("no HIP device visible; the MI355X path has no CPU fallback")
+        arr = (ctypes.c_int * len(devices))(*devices)
+        self.m = self.lib.edc_create_multi(arr, len(devices))
+        if not self.m:
+            raise EngineError(f"edc_create_multi({list(devices)}) failed")
+        self.devices = list(devices)
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self.m:
+            self.lib.edc_destroy_multi(self.m)
+            self.m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc < 0:
+            raise EngineError(f"edc error {rc}: {self.lib.edc_multi_last_error(self.m).decode()}")
+        return rc
+
+    def batch_verify(self, vks, sigs, msgs, z_seed, want_check8=False):
+        arena, offs = _arena(msgs)
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            rc = self.lib.edc_multi_batch_verify(self.m, len(vks), b"".join(vks) or b"\0", b"".join(sigs) or b"\0",
+                                                 arena, offs, bytes(z_seed), check8)
+        self._check(rc)
+        return rc, (check8.raw if check8 is not None else None)
+
+    def batch_verify_fallback(self, vks, sigs, msgs, z_seed):
+        """(code, per-item verify_single codes, number invalid, check8)."""
+        n = len(vks)
+        arena, offs = _arena(msgs)
+        check8 = ctypes.create_string_buffer(32)
+        v = ctypes.create_string_buffer(max(n, 1))
+        cnt = ctypes.c_int(0)
+        with self._lock:
+            rc = self.lib.edc_multi_batch_verify_fallback(self.m, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0",
+                                                          arena, offs, bytes(z_seed), v, ctypes.byref(cnt), check8)
+        self._check(rc)
+        return rc, list(v.raw[:n]), cnt.value, check8.raw
 
 
 _default_engine = None

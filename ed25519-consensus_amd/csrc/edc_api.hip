@@ -3,6 +3,7 @@
 #include <string.h>
 #include <string>
 #include <random>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 #include <hip/hip_ext.h>
@@ -1219,6 +1220,151 @@ int edc_synchronize(edc_ctx* ctx) {
   for (Slot& s : ctx->slot)
     if (s.st) CK(hipStreamSynchronize(s.st));
   return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- several GPUs, one process
+// A consensus node calls Verifier::verify once per block (src/batch.rs:149-217). edc_multi
+// splits that one batch over the contexts of several devices: contiguous shards, shard g's z
+// drawn at its global queue indices (z_base = shard start), so every shard evaluates its part of
+// the same batch equation; each device reduces its shard to one partial point (128 bytes), the
+// partials are gathered through the host (they already come back with each shard's verdict) and
+// summed on the first device, then x8 and the identity test. One host thread per device drives
+// its shard; the same device may appear several times (several contexts on one GPU).
+struct edc_multi {
+  std::vector<edc_ctx*> ctx;
+  std::string err;
+};
+
+struct Shard {
+  size_t lo = 0, hi = 0;
+  int rc = 0, bad = 0;
+  uint8_t partial[128] = {};
+};
+
+static void shard_bounds(size_t n, size_t g, std::vector<Shard>& sh) {
+  sh.assign(g, Shard());
+  for (size_t i = 0; i < g; ++i) {
+    sh[i].lo = n * i / g;
+    sh[i].hi = n * (i + 1) / g;
+  }
+}
+
+template <typename F>
+static void on_each_device(edc_multi* M, std::vector<Shard>& sh, F&& f) {
+  std::vector<std::thread> th;
+  for (size_t g = 1; g < sh.size(); ++g) th.emplace_back([&, g] { sh[g].rc = f(M->ctx[g], sh[g]); });
+  sh[0].rc = f(M->ctx[0], sh[0]);
+  for (auto& t : th) t.join();
+}
+
+// shard's part of the batch on its device: staged from the host, then the whole pipeline on
+// slot 0 (so that a fallback can reuse its k, points and grouping), partial point + bad flag
+static int shard_partial(edc_ctx* c, Shard& s, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t* z_seed) {
+  if (hipSetDevice(c->device) != hipSuccess) return EDC_ERR_HIP;
+  const size_t m = s.hi - s.lo;
+  int rc = upload(c, m, vk + 32 * s.lo, sig + 64 * s.lo, msg, msg_off + s.lo);
+  if (rc) return rc;
+  rc = run_batch_sync(c, m, c->vk, c->sig, c->msg, c->off, z_seed, s.lo, nullptr, nullptr, s.partial, &s.bad);
+  return rc < 0 ? rc : 0;
+}
+
+static int multi_batch(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                       const uint64_t* msg_off, const uint8_t* z_seed, uint8_t check8[32], std::vector<Shard>& sh) {
+  shard_bounds(n, M->ctx.size(), sh);
+  on_each_device(M, sh, [&](edc_ctx* c, Shard& s) { return shard_partial(c, s, vk, sig, msg, msg_off, z_seed); });
+  std::vector<uint8_t> parts(128 * sh.size());
+  int bad = 0;
+  for (size_t g = 0; g < sh.size(); ++g) {
+    if (sh[g].rc < 0) {
+      M->err = std::string("device ") + std::to_string(M->ctx[g]->device) + ": " + M->ctx[g]->err;
+      return sh[g].rc;
+    }
+    memcpy(&parts[128 * g], sh[g].partial, 128);
+    bad |= sh[g].bad;
+  }
+  edc_ctx* c0 = M->ctx[0];
+  if (hipSetDevice(c0->device) != hipSuccess) return EDC_ERR_HIP;
+  const int rc = combine_points(c0, sh.size(), parts.data(), bad, check8, nullptr);
+  if (rc < 0) M->err = c0->err;
+  return rc;
+}
+
+extern "C" {
+
+edc_multi* edc_create_multi(const int* devices, int ndev) {
+  if (!devices || ndev < 1 || ndev > 64) return nullptr;
+  edc_multi* M = new edc_multi();
+  for (int i = 0; i < ndev; ++i) {
+    edc_ctx* c = edc_create(devices[i]);
+    if (!c) {
+      edc_destroy_multi(M);
+      return nullptr;
+    }
+    M->ctx.push_back(c);
+  }
+  return M;
+}
+
+void edc_destroy_multi(edc_multi* M) {
+  if (!M) return;
+  for (edc_ctx* c : M->ctx) edc_destroy(c);
+  delete M;
+}
+
+int edc_multi_size(const edc_multi* M) { return M ? (int)M->ctx.size() : 0; }
+
+edc_ctx* edc_multi_context(edc_multi* M, int i) {
+  return (M && i >= 0 && i < (int)M->ctx.size()) ? M->ctx[i] : nullptr;
+}
+
+const char* edc_multi_last_error(const edc_multi* M) { return M ? M->err.c_str() : "null context"; }
+
+int edc_multi_batch_verify(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                           const uint64_t* msg_off, const uint8_t z_seed[32], uint8_t check8[32]) {
+  if (!M || !z_seed || (n && (!vk || !sig || !msg_off))) return EDC_ERR_ARG;
+  std::vector<Shard> sh;
+  return multi_batch(M, n, vk, sig, msg, msg_off, z_seed, check8, sh);
+}
+
+int edc_multi_batch_verify_fallback(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t* sig,
+                                    const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
+                                    uint8_t* verdicts, int* n_invalid, uint8_t check8[32]) {
+  if (!M || !z_seed || (n && (!vk || !sig || !msg_off || !verdicts))) return EDC_ERR_ARG;
+  if (n_invalid) *n_invalid = 0;
+  std::vector<Shard> sh;
+  const int rc = multi_batch(M, n, vk, sig, msg, msg_off, z_seed, check8, sh);
+  if (rc <= 0) {
+    if (rc == 0 && n) memset(verdicts, 0, n);
+    return rc;
+  }
+  // every shard whose own partial fails (or that saw a decode / canonicity failure) localizes its
+  // invalid items with the grouped fallback, reusing its batch state; the others are all valid
+  on_each_device(M, sh, [&](edc_ctx* c, Shard& s) -> int {
+    const size_t m = s.hi - s.lo;
+    memset(verdicts + s.lo, 0, m);
+    if (hipSetDevice(c->device) != hipSuccess) return EDC_ERR_HIP;
+    const int ok = combine_points(c, 1, s.partial, s.bad, nullptr, nullptr);
+    if (ok <= 0) return ok;
+    Slot& sl = c->slot[0];
+    bool per_sig;
+    uint32_t keys;
+    int r = slot_grouping(c, sl, &per_sig, &keys);
+    if (r) return r;
+    return fallback_ranges(c, sl, m, c->vk, c->sig, c->msg, c->off, z_seed, s.lo, per_sig, keys, verdicts + s.lo);
+  });
+  int total = 0;
+  for (size_t g = 0; g < sh.size(); ++g) {
+    if (sh[g].rc < 0) {
+      M->err = std::string("device ") + std::to_string(M->ctx[g]->device) + ": " + M->ctx[g]->err;
+      return sh[g].rc;
+    }
+    total += sh[g].rc;
+  }
+  if (n_invalid) *n_invalid = total;
+  return EDC_INVALID_SIGNATURE;
 }
 
 }  // extern "C"

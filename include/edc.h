@@ -280,6 +280,33 @@ const char* edc_timing_name(int i);
 /* Synchronize the context stream (for callers that time around device calls). */
 int edc_synchronize(edc_ctx* ctx);
 
+/*
+ * Several GPUs in one process (a node verifying each block's votes across all of its MI355X):
+ * one batch::Verifier::verify (reference src/batch.rs:149-217) split into contiguous shards, one
+ * per listed device (a device may be listed more than once: several contexts on one GPU). Shard g
+ * draws its z at its global queue indices, evaluates its part of the batch equation to one
+ * partial point (128 bytes); the partials are gathered through the host and combined on the
+ * first device (x8, identity). Verdicts and check8 are bit-identical to edc_batch_verify on one
+ * device for any device list. Host buffers as edc_batch_verify; synchronous.
+ */
+typedef struct edc_multi edc_multi;
+edc_multi* edc_create_multi(const int* devices, int ndev);
+void edc_destroy_multi(edc_multi* m);
+int edc_multi_size(const edc_multi* m);
+/* per-device context i (e.g. to load the validator-key cache on every device) */
+edc_ctx* edc_multi_context(edc_multi* m, int i);
+const char* edc_multi_last_error(const edc_multi* m);
+int edc_multi_batch_verify(edc_multi* m, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                           const uint64_t* msg_off, const uint8_t z_seed[32], uint8_t check8[32]);
+/*
+ * edc_multi_batch_verify and, on failure, the grouped fallback on every shard whose own partial
+ * fails (edc_batch_verify_fallback_device semantics): verdicts (host, n bytes) = Item::verify_single
+ * codes, *n_invalid their count. Returns EDC_OK / EDC_INVALID_SIGNATURE / <0.
+ */
+int edc_multi_batch_verify_fallback(edc_multi* m, size_t n, const uint8_t* vk, const uint8_t* sig,
+                                    const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
+                                    uint8_t* verdicts, int* n_invalid, uint8_t check8[32]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -848,3 +848,40 @@ double oc_baseline(size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_
   free(th);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* Small-batch timing on the calling thread (the shape of reference benches/bench.rs:25-71): reps x
+   (queue + verify) of one n-item batch, or reps x (VerificationKey::try_from + verify) of every item
+   ("Unbatched verification"). Seconds; *all_ok = every run accepted. CPU baseline only. */
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+double oc_bench_batch(size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                      int reps, int* all_ok) {
+  oc_init_once();
+  uint8_t seed[32];
+  int ok = 1;
+  const double t0 = now_s();
+  for (int r = 0; r < reps; ++r) {
+    for (int i = 0; i < 32; ++i) seed[i] = (uint8_t)(r * 7 + i);
+    ok &= oc_batch_verify_range(n, vk, sig, msg, off, seed, NULL, 0, NULL, NULL) == OC_OK;
+  }
+  const double t = now_s() - t0;
+  if (all_ok) *all_ok = ok;
+  return t;
+}
+
+double oc_bench_single(size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
+                       int reps, int* all_ok) {
+  oc_init_once();
+  int ok = 1;
+  const double t0 = now_s();
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = 0; i < n; ++i)
+      ok &= oc_verify(vk + 32 * i, sig + 64 * i, msg + off[i], (size_t)(off[i + 1] - off[i])) == OC_OK;
+  const double t = now_s() - t0;
+  if (all_ok) *all_ok = ok;
+  return t;
+}

@@ -25,6 +25,9 @@ def lib():
         L.oc_combine_affine.argtypes = [c_sz, c_p, ctypes.c_void_p]
         L.oc_baseline.restype = ctypes.c_double
         L.oc_baseline.argtypes = [c_sz, c_p, c_p, c_p, u64p, ctypes.c_int, c_sz, ctypes.POINTER(ctypes.c_int)]
+        for f in (L.oc_bench_batch, L.oc_bench_single):
+            f.restype = ctypes.c_double
+            f.argtypes = [c_sz, c_p, c_p, c_p, u64p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -111,3 +114,19 @@ def baseline_c3(n_sample=8192, keys=150, msg_len=120, data=None, min_seconds=1.5
                       f"{f'{msg_len}-byte' if msg_len >= 0 else '0..1024-byte'} msgs), "
                       f"one Verifier per thread over {threads} equal chunks, queue+verify timed, "
                       f"{reps} repeats ({round(total * threads, 1)} CPU-seconds)"}
+
+
+def bench_small(vks, sigs, msgs, batched, min_seconds=0.3):
+    """One-thread rate (sigs/s) of queue+verify of this batch (batched) or of per-item
+    try_from+verify (unbatched), repeated until min_seconds -- reference benches/bench.rs:25-71."""
+    arena, offs = _arena(msgs)
+    f = lib().oc_bench_batch if batched else lib().oc_bench_single
+    ok = ctypes.c_int(0)
+    reps, secs = 1, 0.0
+    while True:
+        secs = f(len(vks), b"".join(vks), b"".join(sigs), arena, offs, reps, ctypes.byref(ok))
+        if secs >= min_seconds or reps >= 1 << 20:
+            break
+        reps = max(reps * 2, int(reps * min_seconds / max(secs, 1e-6)))
+    return {"sigs_per_s": round(reps * len(vks) / secs, 1), "reps": reps, "seconds": round(secs, 3),
+            "ok": bool(ok.value)}

@@ -1,0 +1,70 @@
+"""GPU: the in-process multi-device C ABI (include/edc.h edc_create_multi, the drop-in for one
+batch::Verifier::verify over all of a node's GPUs; reference src/batch.rs:149-217), rehearsed on
+the one-GPU box with the same device listed several times (one context each). For every golden
+batch and device list: verdict and compressed [8]*check equal the fixture (the single-device
+result) bit-exactly, and the sharded fallback gives Item::verify_single's code for every item.
+At configs[2]/[3] scale: a valid 2^20-vote batch is Ok with [8]*check = identity, and with the
+ZIP215 corpus + one bad signature mixed in exactly the bad item is flagged."""
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import ROOT, golden
+
+pytestmark = pytest.mark.gpu
+
+IDENTITY = bytes([1]) + bytes(31)
+
+
+def _items(b):
+    return [(bytes.fromhex(v), bytes.fromhex(s), bytes.fromhex(m)) for v, s, m in b["items"]]
+
+
+@pytest.fixture(scope="module", params=[[0], [0, 0], [0, 0, 0], [0, 0, 0, 0]], ids=lambda d: f"dev{len(d)}")
+def multi(edc, engine, request):
+    m = edc.MultiEngine(request.param)
+    yield m
+    m.close()
+
+
+@pytest.mark.parametrize("b", golden("batches.json")["batches"], ids=lambda b: b["name"])
+def test_multi_batch_fixture(multi, b):
+    it = _items(b)
+    vks, sigs, msgs = [v for v, _, _ in it], [s for _, s, _ in it], [m for _, _, m in it]
+    zs = bytes.fromhex(b["z_seed"])
+    code, c8 = multi.batch_verify(vks, sigs, msgs, zs, want_check8=True)
+    assert code == b["expect_code"]
+    if b["expect_check8"] is not None:
+        assert c8.hex() == b["expect_check8"]
+    code, verdicts, cnt, c8 = multi.batch_verify_fallback(vks, sigs, msgs, zs)
+    assert code == b["expect_code"]
+    exp = b["expect_single"] if code else [0] * len(it)
+    assert verdicts == exp and cnt == sum(1 for e in exp if e)
+
+
+def test_multi_config3_scale(multi, engine):
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    fx = golden("zip215_small_order.json")
+    pkg = sys.modules["ed25519_consensus_amd"]
+    vk, sig, msg, off, expect, _ = bench.make_c4_workload(pkg, engine, torch, dev, n, 150, 120, fx["cases"],
+                                                          bytes.fromhex(fx["msg"]))
+    hv, hs, hm, ho = vk[:32 * n].cpu().numpy().tobytes(), sig[:64 * n].cpu().numpy().tobytes(), \
+        msg.cpu().numpy().tobytes(), off.cpu().tolist()
+    vks = [hv[32 * i:32 * i + 32] for i in range(n)]
+    sigs = [hs[64 * i:64 * i + 64] for i in range(n)]
+    msgs = [hm[ho[i]:ho[i + 1]] for i in range(n)]
+    zs = bytes([0x33]) * 32
+    code, verdicts, cnt, c8 = multi.batch_verify_fallback(vks, sigs, msgs, zs)
+    assert code == 1 and cnt == len(expect)
+    assert {i: v for i, v in enumerate(verdicts) if v} == expect
+    bad = next(iter(expect))
+    keep = [i for i in range(n) if i != bad]
+    code, c8 = multi.batch_verify([vks[i] for i in keep], [sigs[i] for i in keep], [msgs[i] for i in keep], zs,
+                                  want_check8=True)
+    assert code == 0 and c8 == IDENTITY
