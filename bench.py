@@ -169,6 +169,7 @@ def main():
                     help="weak: every rank verifies --n signatures of one global batch; strong: the ranks split "
                          "one batch of --n signatures (n/G each)")
     ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
+    ap.add_argument("--msm-parts", type=int, default=0, help="MSM parts per batch (0 = chosen from the batch size)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -247,7 +248,7 @@ def main():
     if args.keycache and args.keys > 0:           # a node's known validator set, registered once
         kb = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
         eng.keycache_load([kb[32 * i:32 * i + 32] for i in range(len(kb) // 32)])
-    eng._check(lib.edc_set_window_bits(eng.ctx, args.window_bits))
+    eng._check(lib.edc_set_msm_shape(eng.ctx, args.window_bits, args.msm_parts))
     eng._check(lib.edc_reserve(eng.ctx, n))        # every in-flight slot's workspace, before any step
     run_steps(args.warmup)
     if dist:

@@ -93,7 +93,8 @@ struct edc_ctx {
   bool have_key_ratio = false;  // a grouped batch has completed on this context
   double last_key_ratio = 0.0;  // distinct keys / signatures of the last grouped batch
   int ungrouped_run = 0;        // consecutive ungrouped batches since the last grouped one
-  int win_bits = 0;             // MSM window width override (edc_set_window_bits), 0 = by batch size
+  int win_bits = 0;             // MSM window width override (edc_set_msm_shape), 0 = by batch size
+  uint32_t msm_parts = 0;       // MSM parts override (edc_set_msm_shape), 0 = by batch size
   uint64_t secret = 0;          // key-grouping hash secret (OS randomness, per context)
   uint64_t nbatches = 0;
   // grouped fallback (range MSM) staging, slot 0 only
@@ -255,28 +256,33 @@ static int auto_window_bits(size_t n) {
   return 10;
 }
 
-// short windows of c bits over the 128-bit z, then windows of hi bits up to 254 (the top window
-// absorbs the last carry of a 253-bit scalar)
+// Windows of at most c bits over the 128 bits of a z (short scalars: windows 0..ws-1, the top
+// one unsigned since nothing sits above it), then windows of at most hi bits over bits 128..254 of
+// the full-width coefficients (< l < 2^253: bit 253 and 254 are zero, so the top signed digit never
+// carries out). Widths are balanced: a window with only a few live bits would send every term's
+// digit to a handful of buckets of one bin, i.e. one workgroup.
 static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
   MsmPlan P{};
   uint32_t w = 0, off = 0, bin = 0;
-  const uint32_t ws = (128 + c - 1) / c;
-  for (; w < ws; ++w, off += c) {
+  auto add = [&](uint32_t bits, uint32_t buckets) {
     P.off[w] = (uint16_t)off;
-    P.bits[w] = (uint8_t)c;
-    uint32_t buckets = 1u << (c - 1);
-    if (w + 1 == ws && (uint32_t)c * ws == 128) buckets = 1u << c;   // unsigned top digit of a z
+    P.bits[w] = (uint8_t)bits;
     P.nslice[w] = (uint16_t)((buckets + NSLICE - 1) / NSLICE);
     P.bin0[w] = (uint16_t)bin;
     bin += P.nslice[w];
+    off += bits;
+    ++w;
+  };
+  const uint32_t ws = (128 + c - 1) / c;
+  for (uint32_t i = 0; i < ws; ++i) {
+    const uint32_t bits = 128 / ws + (i < 128 % ws ? 1 : 0);
+    add(bits, i + 1 == ws ? (1u << bits) : (1u << (bits - 1)));   // top: unsigned digit up to 2^bits
   }
   P.nwin_short = ws;
-  for (; off < 254; ++w, off += hi) {
-    P.off[w] = (uint16_t)off;
-    P.bits[w] = (uint8_t)hi;
-    P.nslice[w] = (uint16_t)(((1u << (hi - 1)) + NSLICE - 1) / NSLICE);
-    P.bin0[w] = (uint16_t)bin;
-    bin += P.nslice[w];
+  const uint32_t wh = (127 + hi - 1) / hi;
+  for (uint32_t i = 0; i < wh; ++i) {
+    const uint32_t bits = 127 / wh + (i < 127 % wh ? 1 : 0);
+    add(bits, 1u << (bits - 1));
   }
   P.nwin = w;
   P.nranges = nranges;
@@ -287,11 +293,33 @@ static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
 // Batch plan: few distinct keys (consensus votes; known from the previous grouped batch on this
 // context) put the 253-bit B / key coefficients' high bits in 8-bit windows with ~m entries each
 // (one bin per window instead of 128 nearly empty ones); otherwise every window has c bits.
+// Small batches are split into parts (summed per window) so that ~1-2k workgroups accumulate.
 // Any plan is an exact MSM: the hint only affects speed.
 static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
   const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
   const bool few = !per_sig && ctx->have_key_ratio && ctx->last_key_ratio * 16.0 <= 1.0 && n >= 4096;
-  return make_plan(c, few ? 8 : c, 1);
+  MsmPlan P = make_plan(c, few ? 8 : c, 1);
+  uint32_t parts = ctx->msm_parts;
+  if (!parts) {
+    const double entries = (double)n * (few ? P.nwin_short : P.nwin_short + P.nwin);
+    parts = 1;
+    while (parts < 16 && P.bins_per_range * parts * 2 <= 2048 &&
+           entries / ((double)P.bins_per_range * parts * 2) >= 1024.0)
+      parts *= 2;
+  }
+  while (parts > 1 && P.bins_per_range * parts > MSM_MAX_BINS) parts /= 2;
+  P.nranges = parts;
+  P.sum_ranges = parts > 1;
+  return P;
+}
+
+static MsmTerms batch_terms(const MsmPlan& P, const Slot& s, uint32_t n) {
+  MsmTerms T{n, 0, 0, 0, 0, 1, s.scal, nullptr, nullptr, nullptr};
+  if (P.sum_ranges) {
+    T.nparts = P.nranges;
+    T.psize = (uint32_t)((1ull + 2ull * n + P.nranges - 1) / P.nranges);
+  }
+  return T;
 }
 
 // host-staging buffers (inputs of the host-pointer entry points, per-item outputs)
@@ -488,10 +516,8 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
               per_sig);
   mark(PH_MSM_BIN);
-  if (with_bin) {
-    const MsmTerms terms{N, 0, 0, 0, s.scal, nullptr, nullptr, nullptr};
-    launch_msm_bin(st, *P, terms, 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries, s.flags);
-  }
+  if (with_bin) launch_msm_bin(st, *P, batch_terms(*P, s, N), 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries,
+                              s.flags);
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
@@ -934,7 +960,7 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   hipStream_t st = s.st;
   launch_range_coef(st, (uint32_t)n, (uint32_t)rsize, G, m, per_sig, d_sig, s.k, nullptr, seed, z_base, s.key_index,
                     s.scal, s.key_acc, s.u_acc, s.flags, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal);
-  const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, s.scal, ctx->fb_xpt, ctx->fb_xrg,
+  const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 0, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
                        ctx->fb_xscal};
   launch_msm_bin(st, P, terms, npoint + (uint32_t)nx, s.counts, s.offsets, s.cursor, s.entries, s.flags);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
@@ -1179,9 +1205,10 @@ int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits) {
   return 0;
 }
 
-int edc_set_window_bits(edc_ctx* ctx, int bits) {
-  if (!ctx || bits < 0 || (bits && (bits < 8 || bits > 16))) return EDC_ERR_ARG;
+int edc_set_msm_shape(edc_ctx* ctx, int bits, int parts) {
+  if (!ctx || bits < 0 || (bits && (bits < 8 || bits > 16)) || parts < 0 || parts > 64) return EDC_ERR_ARG;
   ctx->win_bits = bits;
+  ctx->msm_parts = (uint32_t)parts;
   return 0;
 }
 
@@ -1189,7 +1216,10 @@ int edc_reserve(edc_ctx* ctx, size_t n) {
   if (!ctx) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
   const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
-  const MsmPlan dense = make_plan(c, c, 1), few = make_plan(c, 8, 1);
+  MsmPlan dense = make_plan(c, c, 1), few = make_plan(c, 8, 1);
+  dense.nranges = few.nranges = MSM_MAX_BINS / (dense.bins_per_range > few.bins_per_range ? dense.bins_per_range
+                                                                                          : few.bins_per_range);
+  if (dense.nranges > 16) dense.nranges = few.nranges = 16;
   const size_t e1 = msm_entry_capacity(dense, n, n + 1), e2 = msm_entry_capacity(few, n, n + 1);
   for (Slot& s : ctx->slot) {
     if (s.pending) { ctx->err = "reserve with a batch in flight"; return EDC_ERR_ARG; }

@@ -84,7 +84,8 @@ constexpr uint32_t MSM_MAX_BINS = 8192;
 
 struct MsmPlan {
   uint32_t nwin, nwin_short;
-  uint32_t nranges;
+  uint32_t nranges;               // ranges (grouped fallback) or parts of one batch (sum_ranges)
+  uint32_t sum_ranges;            // 1: the ranges are parts of ONE MSM, summed per window
   uint32_t bins_per_range;        // sum of nslice over the windows
   uint16_t off[MSM_MAX_WIN];      // first scalar bit of window w
   uint8_t bits[MSM_MAX_WIN];      // width of window w (<= 16)
@@ -93,12 +94,14 @@ struct MsmPlan {
   __host__ __device__ uint32_t nbin() const { return nranges * bins_per_range; }
 };
 
-// The terms of one MSM. Batch (rsize = 0): point terms t = 0..n+m (B, R_i, keys), range 0.
+// The terms of one MSM. Batch (rsize = 0): point terms t = 0..n+m (B, R_i, keys), in part
+// t / psize (parts only spread a small batch over more workgroups; their sums are added per window).
 // Ranges (grouped fallback, rsize > 0): point terms t < npoint are R_i (t < n, point 1+t, range
 // t / rsize) and, for one key term per signature, A_i (point 1+t, range (t-n) / rsize); then nx
 // listed terms (point xpt, range xrg, scalar xscal): the per-(range, key) and per-range B terms.
 struct MsmTerms {
   uint32_t n, rsize, npoint, nx;
+  uint32_t psize, nparts;         // batch split into nparts parts of psize terms (psize 0: one part)
   const uint32_t* scal;
   const uint32_t* xpt;
   const uint32_t* xrg;

@@ -18,7 +18,6 @@
 
 namespace edc {
 
-constexpr int CNT_TERMS_PER_BLOCK = 4096;   // terms per count/scatter workgroup
 
 __device__ __forceinline__ uint32_t terms_count(const MsmTerms& T, const int* flags) {
   return T.rsize ? T.npoint + T.nx : msm_num_points(T.n, (uint32_t)flags[FLAG_NKEYS]);
@@ -30,7 +29,7 @@ __device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t
   const uint32_t* src;
   if (!T.rsize) {
     pt = t;
-    rg = 0;
+    rg = T.psize ? min(t / T.psize, T.nparts - 1) : 0;
     shrt = t >= 1 && t <= T.n;
     src = T.scal + (size_t)t * 8;
   } else if (t < T.npoint) {       // R_i (t < n), then one key term per signature
@@ -65,15 +64,15 @@ __device__ __forceinline__ void term_digits(const MsmPlan& P, bool shrt, uint32_
   }
 }
 
-__global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32_t* __restrict__ counts,
-                                                   const int* __restrict__ flags) {
+__global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32_t per_block,
+                                                   uint32_t* __restrict__ counts, const int* __restrict__ flags) {
   extern __shared__ uint32_t hist[];
   const uint32_t nbin = P.nbin();
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   const uint32_t cnt = terms_count(T, flags);
-  const uint32_t t0 = blockIdx.x * CNT_TERMS_PER_BLOCK;
-  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+  const uint32_t t0 = blockIdx.x * per_block;
+  for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
     const uint32_t t = t0 + u;
     if (t >= cnt) break;
     uint32_t pt, rg, s[8];
@@ -112,8 +111,9 @@ __global__ void __launch_bounds__(1024) k_msm_scan(uint32_t nbin, const uint32_t
   }
 }
 
-__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint32_t* __restrict__ cursor,
-                                                     uint2* __restrict__ entries, const int* __restrict__ flags) {
+__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint32_t per_block,
+                                                     uint32_t* __restrict__ cursor, uint2* __restrict__ entries,
+                                                     const int* __restrict__ flags) {
   extern __shared__ uint32_t smem_hist[];
   const uint32_t nbin = P.nbin();
   uint32_t* hist = smem_hist;
@@ -121,9 +121,9 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   const uint32_t cnt = terms_count(T, flags);
-  const uint32_t t0 = blockIdx.x * CNT_TERMS_PER_BLOCK;
+  const uint32_t t0 = blockIdx.x * per_block;
   // pass 1: local counts (recomputed in pass 2 from the same digits)
-  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+  for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
     const uint32_t t = t0 + u;
     if (t >= cnt) break;
     uint32_t pt, rg, s[8];
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     hist[b] = 0;
   }
   __syncthreads();
-  for (uint32_t u = threadIdx.x; u < CNT_TERMS_PER_BLOCK; u += blockDim.x) {
+  for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
     const uint32_t t = t0 + u;
     if (t >= cnt) break;
     uint32_t pt, rg, s[8];
@@ -418,23 +418,37 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
   }
 }
 
-// Win(range g, window w) = sum_s W_s + 256 * sum_s s T_s over the window's slices (windows with
-// more than one slice; they form a prefix of the plan). One workgroup per (range, window).
-__global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, uint32_t nmulti, const uint32_t* __restrict__ slice_W,
+// Win(range g, window w) = sum_s W_s + 256 * sum_s s T_s over the window's slices, for windows
+// with more than one slice (single-slice windows are read straight from their bin). One
+// workgroup per (range, window).
+__global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* __restrict__ slice_W,
                                                     const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t g = blockIdx.x / P.nwin, w = blockIdx.x % P.nwin;
+  const uint32_t ns = P.nslice[w];
+  if (ns <= 1 && !P.sum_ranges) return;
   __builtin_amdgcn_s_setprio(3);   // latency-bound tail: issue ahead of co-resident bulk waves
   const int t = threadIdx.x;
-  const uint32_t g = blockIdx.x / nmulti, w = blockIdx.x % nmulti;
-  const uint32_t ns = P.nslice[w];
   const uint32_t b0 = g * P.bins_per_range + P.bin0[w];
+  // slice t's sums; parts of one batch (sum_ranges) are added first
+  ge_p3 sT = ge_identity(), sW = ge_identity();
+  if ((uint32_t)t < ns) {
+    sT = ld_ext(slice_T + (size_t)(b0 + t) * EXT_WORDS);
+    sW = ld_ext(slice_W + (size_t)(b0 + t) * EXT_WORDS);
+    if (P.sum_ranges)
+      for (uint32_t p = 1; p < P.nranges; ++p) {
+        const size_t b = (size_t)p * P.bins_per_range + P.bin0[w] + t;
+        sT = ge_add(sT, ld_ext(slice_T + b * EXT_WORDS));
+        sW = ge_add(sW, ld_ext(slice_W + b * EXT_WORDS));
+      }
+  }
   uint32_t* lpts = smem;
-  st_ext(lpts + t * EXT_WORDS, (uint32_t)t < ns ? ld_ext(slice_T + (size_t)(b0 + t) * EXT_WORDS) : ge_identity());
+  st_ext(lpts + t * EXT_WORDS, sT);
   __syncthreads();
   ge_p3 ws, tot;
   weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
   __syncthreads();
-  ge_p3 a = sum_256((uint32_t)t < ns ? ld_ext(slice_W + (size_t)(b0 + t) * EXT_WORDS) : ge_identity(), lpts);
+  ge_p3 a = sum_256(sW, lpts);
   if (t < 4) {
     ge_p3 x = ws;
     for (int k = 0; k < SLICE_BITS; ++k) x = quad_dbl(x);
@@ -495,7 +509,7 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
 // window sum of (range g, window w): combined by k_msm_window, or the single bin's W
 __device__ __forceinline__ ge_p3 window_sum(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* slice_W,
                                              const uint32_t* win) {
-  if (P.nslice[w] > 1) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
+  if (P.nslice[w] > 1 || P.sum_ranges) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
   return ld_ext(slice_W + (size_t)(g * P.bins_per_range + P.bin0[w]) * EXT_WORDS);
 }
 
@@ -559,11 +573,15 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags) {
   const uint32_t nbin = P.nbin();
   (void)hipMemsetAsync(counts, 0, nbin * sizeof(uint32_t), st);
-  const uint32_t grid = cdiv(max_terms ? max_terms : 1, CNT_TERMS_PER_BLOCK);
-  hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, counts, flags);
+  // terms per workgroup: up to 4096 (long runs of entries per bin for the scatter's writes), but
+  // at least ~256 workgroups so small batches still fill the GPU
+  uint32_t per = max_terms / 256;
+  per = per < 256 ? 256 : (per > 4096 ? 4096 : (per + 255) / 256 * 256);
+  const uint32_t grid = cdiv(max_terms ? max_terms : 1, per);
+  hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
-  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), 2 * nbin * sizeof(uint32_t), st, P, T, cursor, entries,
-                     flags);
+  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), 2 * nbin * sizeof(uint32_t), st, P, T, per, cursor,
+                     entries, flags);
 }
 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
@@ -578,24 +596,23 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
 
 size_t msm_bucket_words(uint32_t nbin) { return (size_t)nbin * NSLICE * EXT_WORDS; }
 
-static uint32_t plan_nmulti(const MsmPlan& P) {
-  uint32_t k = 0;
-  while (k < P.nwin && P.nslice[k] > 1) ++k;
-  return k;
+static bool plan_multi(const MsmPlan& P) {
+  for (uint32_t w = 0; w < P.nwin; ++w)
+    if (P.nslice[w] > 1) return true;
+  return false;
 }
 
 void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out) {
-  const uint32_t nm = plan_nmulti(P);
-  if (nm) hipLaunchKernelGGL(k_msm_window, dim3(nm), dim3(256), kReduceLds, st, P, nm, slice_W, slice_T, win);
+  if (plan_multi(P) || P.sum_ranges)
+    hipLaunchKernelGGL(k_msm_window, dim3(P.nwin), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
   hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, P, slice_W, win, flags, want_compress, out);
 }
 
 void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                            uint32_t* win, uint8_t* rverdict) {
-  const uint32_t nm = plan_nmulti(P);
-  if (nm)
-    hipLaunchKernelGGL(k_msm_window, dim3(nm * P.nranges), dim3(256), kReduceLds, st, P, nm, slice_W, slice_T, win);
+  if (plan_multi(P))
+    hipLaunchKernelGGL(k_msm_window, dim3(P.nwin * P.nranges), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
   hipLaunchKernelGGL(k_msm_range_final, dim3(cdiv(4ull * P.nranges, 64)), dim3(64), 0, st, P, slice_W, win,
                      rverdict);
 }

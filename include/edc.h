@@ -250,10 +250,11 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
 int edc_set_key_grouping(edc_ctx* ctx, int mode);
 
 /*
- * Pippenger window width for this context's batches: 0 (default) picks it from the batch size;
- * 8..16 forces it (tuning / measurement). Results never depend on it.
+ * Pippenger shape for this context's batches (tuning / measurement): window width `bits` (8..16)
+ * and number of parts a batch's terms are split into (1..64; parts are summed per window). 0 for
+ * either picks it from the batch size (default). Results never depend on it.
  */
-int edc_set_window_bits(edc_ctx* ctx, int bits);
+int edc_set_msm_shape(edc_ctx* ctx, int bits, int parts);
 
 /*
  * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous

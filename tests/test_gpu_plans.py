@@ -3,7 +3,8 @@ the C oracle (dalek algorithm: Straus below 190 terms, Pippenger w = 6/7/8 above
 compressed [8]*check, bit-exact, for valid batches and for batches whose check point is NOT the
 identity (one bad item).
 
-Plans covered: window widths 9..16 and the size-chosen default; 8-bit high windows for the B / key
+Plans covered: window widths 9..16 and the size-chosen default, one batch split into 1..16
+parts (summed per window); 8-bit high windows for the B / key
 coefficients (chosen when the previous grouped batch on the context had few distinct keys) and
 full-width windows otherwise; grouped keys, one key term per signature, and the on-device overflow
 path of key grouping (set_key_grouping(3): grouping abandoned mid-batch, as adversarial keys would
@@ -39,19 +40,19 @@ def _batch(engine, n, m, bad, msg_len=120, seed=0):
 
 @pytest.mark.parametrize("n,m,bad", [(4096, 256, None), (4096, 256, 77), (4096, 257, 5), (8192, 5, 8000),
                                      (8192, 1, None), (8192, 150, 3), (6000, 6000, 17)])
-@pytest.mark.parametrize("bits", [0, 9, 12, 16])
-def test_plans_match_oracle(engine, oracle_c, n, m, bad, bits):
+@pytest.mark.parametrize("bits,parts", [(0, 0), (9, 1), (12, 3), (13, 0), (16, 1), (16, 2), (11, 16)])
+def test_plans_match_oracle(engine, oracle_c, n, m, bad, bits, parts):
     vks, sigs, msgs, zseed = _batch(engine, n, m, bad)
     exp_code, exp_c8 = oracle_c.batch_verify(list(zip(vks, sigs, msgs)), zseed)
     assert exp_code == (0 if bad is None else 1)
-    engine.set_window_bits(bits)
+    engine.set_msm_shape(bits, parts)
     try:
         for _ in range(2):
             code, c8 = engine.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True)
             assert code == exp_code
             assert c8 == exp_c8
     finally:
-        engine.set_window_bits(0)
+        engine.set_msm_shape(0, 0)
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3])

@@ -89,6 +89,113 @@ __global__ void __launch_bounds__(256, W) k_sqr_nop(uint32_t* out, unsigned long
   stamp(clk, t0, r0);
 }
 
+// ---- full-radix alternative (north star: "64-bit-limb arithmetic"): 4 x 64-bit limbs held as
+// 8 x 32-bit words, value < 2^256, mod p via 2^256 == 38. Comba columns of the 28 cross products
+// accumulate in 64 bits with the carry-out of every v_mad_u64_u32 counted by a v_addc_co_u32
+// (the carry-in-mad trick of radix 2^29 is impossible: full 32-bit limbs overflow a 64-bit
+// column), then doubling, the 8 squares and the 38-fold.
+__device__ __forceinline__ uint64_t mad_cc(uint32_t a, uint32_t b, uint64_t c, uint32_t& cnt) {
+  uint64_t d;
+  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %4\n\tv_addc_co_u32 %1, vcc, 0, %1, vcc"
+               : "=&v"(d), "+v"(cnt) : "v"(a), "v"(b), "v"(c) : "vcc");
+  return d;
+}
+
+struct fe32 { uint32_t w[8]; };
+
+__device__ __forceinline__ fe32 sqr_r32(const fe32& x) {
+  const uint32_t* a = x.w;
+  uint32_t t[16];
+  // cross products sum_{i<j} a_i a_j, column by column (96-bit running value cnt:acc)
+  uint64_t acc = 0;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 1; k < 14; ++k) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int j = k - i;
+      if (j > i && j < 8) acc = mad_cc(a[i], a[j], acc, cnt);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)cnt << 32);
+    cnt = 0;
+  }
+  t[0] = 0;
+  t[14] = (uint32_t)acc;
+  t[15] = (uint32_t)(acc >> 32);
+  // double, then add the squares a_i^2 at columns 2i, 2i+1
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 15; k >= 1; --k) t[k] = (t[k] << 1) | (t[k - 1] >> 31);
+  t[0] = 0;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t p = (uint64_t)a[i] * a[i];
+    uint64_t lo = (uint64_t)t[2 * i] + (uint32_t)p + (c & 0xFFFFFFFFull);
+    t[2 * i] = (uint32_t)lo;
+    uint64_t hi = (uint64_t)t[2 * i + 1] + (p >> 32) + (lo >> 32) + (c >> 32);
+    t[2 * i + 1] = (uint32_t)hi;
+    c = hi >> 32;
+  }
+  top = (uint32_t)c;
+  (void)top;
+  // fold: t_lo + 38 t_hi (each mad's addend t_lo + carry < 2^33, result < 2^39)
+  fe32 r;
+  uint64_t f = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    f = mad64(t[8 + i], 38u, (uint64_t)t[i] + (f >> 32));
+    r.w[i] = (uint32_t)f;
+  }
+  // the last carry (< 2^6) once more: 2^256 == 38; a carry out of this pass is folded again
+  uint64_t g = (uint64_t)r.w[0] + (f >> 32) * 38u;
+  r.w[0] = (uint32_t)g;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    g = (uint64_t)r.w[i] + (g >> 32);
+    r.w[i] = (uint32_t)g;
+  }
+  r.w[0] += (uint32_t)(g >> 32) * 38u;
+  return r;
+}
+
+__device__ fe32 seed_fe32(uint32_t s) {
+  fe32 a;
+  for (int i = 0; i < 8; ++i) a.w[i] = s * 2654435761u + i * 40503u;
+  return a;
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, W) k_sqr_r32(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe32 a = seed_fe32(s + blockIdx.x * 256 + threadIdx.x);
+  for (int i = 0; i < ITERS; ++i) a = sqr_r32(a);
+  out[blockIdx.x * 256 + threadIdx.x] = a.w[0] ^ a.w[7];
+  stamp(clk, t0, r0);
+}
+
+// correctness of sqr_r32 against the production radix-2^29 fe_sqr (canonical results compared)
+__global__ void k_check_r32(uint32_t* bad, uint32_t s) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  fe32 a = seed_fe32(s + t);
+  a.w[7] &= 0x7FFFFFFFu;                 // < 2^255: the same value in both representations
+  fe x = fe_from_words(a.w);
+  for (int i = 0; i < 16; ++i) { a = sqr_r32(a); x = fe_sqr(x); }
+  // canonical form of the full-radix value: < 2^256, reduce through radix 2^29 (bit 255 folded as 19)
+  uint32_t w[8], y[8];
+  for (int i = 0; i < 8; ++i) w[i] = a.w[i];
+  const uint32_t b255 = w[7] >> 31;
+  w[7] &= 0x7FFFFFFFu;
+  fe z = fe_from_words(w);
+  z.v[0] += 19u * b255;
+  fe_to_words(z, w);
+  fe_to_words(x, y);
+  uint32_t diff = 0;
+  for (int i = 0; i < 8; ++i) diff |= w[i] ^ y[i];
+  if (diff) atomicAdd(bad, 1u);
+}
+
 typedef void (*kfn)(uint32_t*, unsigned long long*, uint32_t);
 
 // occupancy is pinned with dynamic LDS: w blocks of 256 lanes (one wave per SIMD each) per CU
@@ -131,6 +238,18 @@ int main() {
   run("sqr ilp2 w4", k_sqr2<4>, 4, ITERS, 336, d, clk, blocks);
   run("sqr ilp2 w2", k_sqr2<2>, 2, ITERS, 336, d, clk, blocks);
   run("sqr+16nop w4", k_sqr_nop<4>, 4, ITERS, 336, d, clk, blocks);
+  {
+    uint32_t* bad;
+    CHK(hipMalloc(&bad, 4));
+    CHK(hipMemset(bad, 0, 4));
+    hipLaunchKernelGGL(k_check_r32, dim3(1024), dim3(256), 0, 0, bad, 12345u);
+    uint32_t hb = 0;
+    CHK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+    printf("sqr_r32 vs fe_sqr: %u mismatches of %d (16 chained squarings each)\n", hb, 1024 * 256);
+    CHK(hipFree(bad));
+  }
+  run("sqr_r32 w4", k_sqr_r32<4>, 4, ITERS, 0, d, clk, blocks);
+  run("sqr_r32 w8", k_sqr_r32<8>, 8, ITERS, 0, d, clk, blocks);
   run("mul w4", k_mul<4>, 4, ITERS, 456, d, clk, blocks);
   run("mul w8", k_mul<8>, 8, ITERS, 456, d, clk, blocks);
   CHK(hipFree(d));
