@@ -27,7 +27,7 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, count * sizeof(T));
 }
 
-constexpr int kSlots = 4;  // batches that can be in flight per context
+constexpr int kSlots = 8;  // batches that can be in flight per context
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
 }  // namespace

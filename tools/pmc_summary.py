@@ -12,18 +12,26 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = 1 << 20
-KERNELS = ["k_decompress", "k_challenge", "k_msm_accum_dma"]
+KERNELS = ["k_decompress", "k_challenge", "k_msm_accum_dma", "k_msm_scatter", "k_coef"]
 MAD_CYC, OTHER_CYC, SIMDS = 4.46, 2.5, 1024     # profiles/r01_valu_rates.txt; 256 CU x 4 SIMD
 
 
 def medians(path):
-    """{kernel short name: {counter: median over this kernel's full-size dispatches}}"""
-    per = defaultdict(lambda: defaultdict(list))
+    """{kernel short name: {counter: median over this kernel's dispatches with its largest grid}}
+    (the bench's batch-size launches; the small signing / setup launches have smaller grids)"""
+    rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"].split("(")[0].replace("edc::", "")
-            if name in KERNELS and int(r["Grid_Size"]) >= N // 2:
-                per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if name in KERNELS:
+                rows.append((name, int(r["Grid_Size"]), r["Counter_Name"], float(r["Counter_Value"])))
+    top = {}
+    for name, g, _, _ in rows:
+        top[name] = max(top.get(name, 0), g)
+    per = defaultdict(lambda: defaultdict(list))
+    for name, g, c, v in rows:
+        if g == top[name]:
+            per[name][c].append(v)
     return {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
@@ -38,6 +46,8 @@ def main():
                      "INT64 x 4.46 + (VALU - INT64) x 2.5 cycles (profiles/r01_valu_rates.txt) over 1024 SIMDs.",
            "n": N, "kernels": {}}
     for k in KERNELS:
+        if k not in p["valu"] or k not in p["int"]:
+            continue
         a, b = p["valu"][k], p["int"][k]
         waves, valu, i64 = a["SQ_WAVES"], a["SQ_INSTS_VALU"], b["SQ_INSTS_VALU_INT64"]
         cyc = a["GRBM_GUI_ACTIVE"] / 8
@@ -61,6 +71,21 @@ def main():
                  "128-byte point records"}
     with open(os.path.join(ROOT, "profiles", "traffic_k_decompress.json"), "w") as f:
         json.dump(t, f, indent=1)
+    # MSM traffic: the scatter writes 8-byte entries (8 windows x n R digits at configs[2]); the
+    # accumulation gathers one 112-byte row per entry
+    entries = 8 * N
+    msm = {"n": N, "entries": entries, "entry_bytes": entries * 8,
+           "k_msm_scatter": {"write_bytes": int(p["write"].get("k_msm_scatter", {}).get("WRITE_SIZE", 0) * 1024),
+                             "fetch_bytes": int(p["fetch"].get("k_msm_scatter", {}).get("FETCH_SIZE", 0) * 1024 * 2)},
+           "k_msm_accum_dma": {"fetch_bytes": int(p["fetch"].get("k_msm_accum_dma", {}).get("FETCH_SIZE", 0) * 1024 * 2),
+                               "write_bytes": int(p["write"].get("k_msm_accum_dma", {}).get("WRITE_SIZE", 0) * 1024),
+                               "algorithmic_gather_bytes": entries * 112}}
+    msm["k_msm_scatter"]["write_over_entry_bytes"] = round(msm["k_msm_scatter"]["write_bytes"] / (entries * 8), 3)
+    if "k_msm_accum_dma" in out["kernels"]:
+        msm["k_msm_accum_dma"]["cycles_per_valu_per_simd"] = out["kernels"]["k_msm_accum_dma"]["cycles_per_valu_per_simd"]
+    with open(os.path.join(ROOT, "profiles", "traffic_msm.json"), "w") as f:
+        json.dump(msm, f, indent=1)
+    print(json.dumps(msm, indent=1))
     print(json.dumps(out["kernels"], indent=1))
     print(json.dumps(t, indent=1))
 
