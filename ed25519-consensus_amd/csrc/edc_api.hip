@@ -119,10 +119,13 @@ struct edc_ctx {
   }
 };
 
+// A failed HIP call also leaves the thread's last-error state set; it is cleared here, so that a
+// later hipGetLastError() after a kernel launch reports only that launch.
 #define CK(expr)                                                        \
   do {                                                                  \
     hipError_t e_ = (expr);                                             \
     if (e_ != hipSuccess) {                                             \
+      (void)hipGetLastError();                                          \
       ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);     \
       return EDC_ERR_HIP;                                               \
     }                                                                   \
@@ -605,6 +608,7 @@ edc_ctx* edc_create(int device) {
     std::random_device rd;   // OS randomness: the key-grouping hash secret of this context
     ctx->secret = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
   }
+  (void)hipGetLastError();   // launch checks below must not see an earlier, unrelated failure
   bool ok = hipSetDevice(device) == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
             dalloc(&ctx->btab, BTAB_ENTRIES * NIELS_WORDS) == hipSuccess;
   if (ok) {
@@ -612,7 +616,9 @@ edc_ctx* edc_create(int device) {
     ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->st()) == hipSuccess;
   }
   if (!ok) {
+    (void)hipGetLastError();
     edc_destroy(ctx);
+    (void)hipGetLastError();
     return nullptr;
   }
   return ctx;
