@@ -170,6 +170,7 @@ def main():
                          "one batch of --n signatures (n/G each)")
     ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
     ap.add_argument("--msm-parts", type=int, default=0, help="MSM parts per batch (0 = chosen from the batch size)")
+    ap.add_argument("--bin-entries", type=int, default=0, help="target MSM entries per bin (0 = chosen from the batch size)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -249,6 +250,7 @@ def main():
         kb = bytes(vk[:32 * min(args.keys, n)].cpu().tolist())
         eng.keycache_load([kb[32 * i:32 * i + 32] for i in range(len(kb) // 32)])
     eng._check(lib.edc_set_msm_shape(eng.ctx, args.window_bits, args.msm_parts))
+    eng._check(lib.edc_set_msm_bin_entries(eng.ctx, args.bin_entries))
     eng._check(lib.edc_reserve(eng.ctx, n))        # every in-flight slot's workspace, before any step
     run_steps(args.warmup)
     if dist:

@@ -43,7 +43,7 @@ ABI_SYMBOLS = [
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
     "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
-    "edc_set_msm_shape", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
+    "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
 ]
 
@@ -118,6 +118,7 @@ def load_library(path=None):
         lib.edc_batch_verify_fallback_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_vp,
                                                          ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_set_msm_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
+        lib.edc_set_msm_bin_entries.argtypes = [c_vp, ctypes.c_int]
         lib.edc_set_fallback_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
         lib.edc_create_multi.restype = c_vp
         lib.edc_create_multi.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
@@ -323,6 +324,10 @@ class Engine:
     def set_msm_shape(self, bits=0, parts=0):
         """Pippenger window width (8..16) and parts (1..64); 0 = chosen from the batch size."""
         self._check(self.lib.edc_set_msm_shape(self.ctx, int(bits), int(parts)))
+
+    def set_msm_bin_entries(self, entries=0):
+        """Target MSM entries per bin (>= 256); 0 = chosen from the batch size."""
+        self._check(self.lib.edc_set_msm_bin_entries(self.ctx, int(entries)))
 
     def keycache_clear(self):
         with self._lock:

@@ -94,6 +94,7 @@ struct edc_ctx {
   double last_key_ratio = 0.0;  // distinct keys / signatures of the last grouped batch
   int ungrouped_run = 0;        // consecutive ungrouped batches since the last grouped one
   int win_bits = 0;             // MSM window width override (edc_set_msm_shape), 0 = by batch size
+  uint32_t bin_entries = 0;     // target entries per MSM bin (edc_set_msm_bin_entries), 0 = by batch size
   uint32_t msm_parts = 0;       // MSM parts override (edc_set_msm_shape), 0 = by batch size
   uint64_t secret = 0;          // key-grouping hash secret (OS randomness, per context)
   uint64_t nbatches = 0;
@@ -259,70 +260,101 @@ static int auto_window_bits(size_t n) {
   return 10;
 }
 
-// Windows of at most c bits over the 128 bits of a z (short scalars: windows 0..ws-1, the top
-// one unsigned since nothing sits above it), then windows of at most hi bits over bits 128..254 of
-// the full-width coefficients (< l < 2^253: bit 253 and 254 are zero, so the top signed digit never
-// carries out). Widths are balanced: a window with only a few live bits would send every term's
-// digit to a handful of buckets of one bin, i.e. one workgroup.
+// Windows of at most c bits over the 128 bits of a z (short scalars: windows 0..ws-1), then
+// windows of at most hi bits over bits 128..252 of the full-width coefficients (< l < 2^253). The
+// top window of each kind is unsigned (nothing sits above it, so no carry out): its digit reaches
+// 2^bits, hence 2^bits buckets instead of 2^(bits-1). Widths are balanced: a window with only a
+// few live bits would send every term's digit to a handful of buckets of one bin, i.e. one
+// workgroup. Every slice starts as one bin (nsub = 1; batch_plan may split them).
+static void plan_layout(MsmPlan& P) {
+  uint32_t bin = 0;
+  for (uint32_t w = 0; w < P.nwin; ++w) {
+    P.bin0[w] = (uint16_t)bin;
+    bin += (uint32_t)P.nslice[w] * P.nsub[w];
+  }
+  P.bins_per_range = bin;
+}
+
 static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
   MsmPlan P{};
-  uint32_t w = 0, off = 0, bin = 0;
+  uint32_t w = 0, off = 0;
   auto add = [&](uint32_t bits, uint32_t buckets) {
     P.off[w] = (uint16_t)off;
     P.bits[w] = (uint8_t)bits;
     P.nslice[w] = (uint16_t)((buckets + NSLICE - 1) / NSLICE);
-    P.bin0[w] = (uint16_t)bin;
-    bin += P.nslice[w];
+    P.nsub[w] = 1;
     off += bits;
     ++w;
   };
   const uint32_t ws = (128 + c - 1) / c;
   for (uint32_t i = 0; i < ws; ++i) {
     const uint32_t bits = 128 / ws + (i < 128 % ws ? 1 : 0);
-    add(bits, i + 1 == ws ? (1u << bits) : (1u << (bits - 1)));   // top: unsigned digit up to 2^bits
+    add(bits, i + 1 == ws ? (1u << bits) : (1u << (bits - 1)));
   }
   P.nwin_short = ws;
-  const uint32_t wh = (127 + hi - 1) / hi;
+  const uint32_t wh = (125 + hi - 1) / hi;
   for (uint32_t i = 0; i < wh; ++i) {
-    const uint32_t bits = 127 / wh + (i < 127 % wh ? 1 : 0);
-    add(bits, 1u << (bits - 1));
+    const uint32_t bits = 125 / wh + (i < 125 % wh ? 1 : 0);
+    add(bits, i + 1 == wh ? (1u << bits) : (1u << (bits - 1)));
   }
   P.nwin = w;
   P.nranges = nranges;
-  P.bins_per_range = bin;
+  plan_layout(P);
   return P;
+}
+
+static uint32_t floor_pow2(double x) {
+  uint32_t p = 1;
+  while (p * 2.0 <= x && p < 64) p *= 2;
+  return p;
 }
 
 // Batch plan: few distinct keys (consensus votes; known from the previous grouped batch on this
 // context) put the 253-bit B / key coefficients' high bits in 8-bit windows with ~m entries each
 // (one bin per window instead of 128 nearly empty ones); otherwise every window has c bits.
-// Small batches are split into parts (summed per window) so that ~1-2k workgroups accumulate.
-// Any plan is an exact MSM: the hint only affects speed.
+// Small batches split the slices of their densest windows into sub-bins (terms interleaved by
+// index, summed per slice by k_msm_window) so that every bin holds about the same number of
+// entries and ~1-2k workgroups accumulate. edc_set_msm_shape's parts instead split the whole batch.
+// Any plan is an exact MSM: the hint and the split only affect speed.
 static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
   const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
   const bool few = !per_sig && ctx->have_key_ratio && ctx->last_key_ratio * 16.0 <= 1.0 && n >= 4096;
   MsmPlan P = make_plan(c, few ? 8 : c, 1);
-  uint32_t parts = ctx->msm_parts;
-  if (!parts) {
-    const double entries = (double)n * (few ? P.nwin_short : P.nwin_short + P.nwin);
-    parts = 1;
-    while (parts < 16 && P.bins_per_range * parts * 2 <= 2048 &&
-           entries / ((double)P.bins_per_range * parts * 2) >= 1024.0)
-      parts *= 2;
+  if (ctx->msm_parts) {
+    uint32_t parts = ctx->msm_parts;
+    while (parts > 1 && P.bins_per_range * parts > MSM_MAX_BINS) parts /= 2;
+    P.nranges = parts;
+    P.sum_ranges = parts > 1;
+    return P;
   }
-  while (parts > 1 && P.bins_per_range * parts > MSM_MAX_BINS) parts /= 2;
-  P.nranges = parts;
-  P.sum_ranges = parts > 1;
+  // expected entries per slice of each window: short terms (the z_i) use the short windows, full
+  // terms (B and the keys: m estimated from the last grouped batch, n per signature) all windows.
+  // Only the lower half of two windows' slices is live: in the top short window the full terms'
+  // digits are signed, and in the top full window bit 252 is set only by coefficients in
+  // [2^252, l), a 2^-125 fraction.
+  const double ns = (double)n;
+  const double nf = 1.0 + (per_sig ? ns : (ctx->have_key_ratio ? ctx->last_key_ratio * ns : ns));
+  double dens[MSM_MAX_WIN], total = 0;
+  for (uint32_t w = 0; w < P.nwin; ++w) {
+    const double sl = P.nslice[w], half = sl > 1 ? sl / 2 : 1;
+    if (w + 1 < P.nwin_short) dens[w] = (ns + nf) / sl;
+    else if (w + 1 == P.nwin_short) dens[w] = ns / sl + nf / half;
+    else if (w + 1 < P.nwin) dens[w] = nf / sl;
+    else dens[w] = nf / half;
+    total += (w < P.nwin_short ? ns + nf : nf);
+  }
+  double target = ctx->bin_entries ? (double)ctx->bin_entries : (total / 1024.0 > 4096.0 ? total / 1024.0 : 4096.0);
+  for (;;) {
+    for (uint32_t w = 0; w < P.nwin; ++w) P.nsub[w] = (uint8_t)floor_pow2(dens[w] / target);
+    plan_layout(P);
+    if (P.bins_per_range <= MSM_MAX_BINS) break;
+    target *= 2;
+  }
   return P;
 }
 
 static MsmTerms batch_terms(const MsmPlan& P, const Slot& s, uint32_t n) {
-  MsmTerms T{n, 0, 0, 0, 0, 1, s.scal, nullptr, nullptr, nullptr};
-  if (P.sum_ranges) {
-    T.nparts = P.nranges;
-    T.psize = (uint32_t)((1ull + 2ull * n + P.nranges - 1) / P.nranges);
-  }
-  return T;
+  return MsmTerms{n, 0, 0, 0, P.sum_ranges ? P.nranges : 1u, s.scal, nullptr, nullptr, nullptr};
 }
 
 // host-staging buffers (inputs of the host-pointer entry points, per-item outputs)
@@ -966,7 +998,7 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   hipStream_t st = s.st;
   launch_range_coef(st, (uint32_t)n, (uint32_t)rsize, G, m, per_sig, d_sig, s.k, nullptr, seed, z_base, s.key_index,
                     s.scal, s.key_acc, s.u_acc, s.flags, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal);
-  const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 0, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
+  const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
                        ctx->fb_xscal};
   launch_msm_bin(st, P, terms, npoint + (uint32_t)nx, s.counts, s.offsets, s.cursor, s.entries, s.flags);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
@@ -1215,6 +1247,12 @@ int edc_set_msm_shape(edc_ctx* ctx, int bits, int parts) {
   if (!ctx || bits < 0 || (bits && (bits < 8 || bits > 16)) || parts < 0 || parts > 64) return EDC_ERR_ARG;
   ctx->win_bits = bits;
   ctx->msm_parts = (uint32_t)parts;
+  return 0;
+}
+
+int edc_set_msm_bin_entries(edc_ctx* ctx, int entries) {
+  if (!ctx || entries < 0 || (entries && entries < 256)) return EDC_ERR_ARG;
+  ctx->bin_entries = (uint32_t)entries;
   return 0;
 }
 

@@ -86,22 +86,24 @@ struct MsmPlan {
   uint32_t nwin, nwin_short;
   uint32_t nranges;               // ranges (grouped fallback) or parts of one batch (sum_ranges)
   uint32_t sum_ranges;            // 1: the ranges are parts of ONE MSM, summed per window
-  uint32_t bins_per_range;        // sum of nslice over the windows
+  uint32_t bins_per_range;        // sum of nslice * nsub over the windows
   uint16_t off[MSM_MAX_WIN];      // first scalar bit of window w
   uint8_t bits[MSM_MAX_WIN];      // width of window w (<= 16)
+  uint8_t nsub[MSM_MAX_WIN];      // sub-bins per slice of window w (power of 2; term t -> t mod nsub)
   uint16_t bin0[MSM_MAX_WIN];     // first bin of window w inside a range
   uint16_t nslice[MSM_MAX_WIN];   // slices of window w
   __host__ __device__ uint32_t nbin() const { return nranges * bins_per_range; }
 };
 
 // The terms of one MSM. Batch (rsize = 0): point terms t = 0..n+m (B, R_i, keys), in part
-// t / psize (parts only spread a small batch over more workgroups; their sums are added per window).
+// t mod nparts (parts only spread a small batch over more workgroups; their sums are added per
+// window; interleaved, so that each part holds the same mix of short z_i and full-width terms).
 // Ranges (grouped fallback, rsize > 0): point terms t < npoint are R_i (t < n, point 1+t, range
 // t / rsize) and, for one key term per signature, A_i (point 1+t, range (t-n) / rsize); then nx
 // listed terms (point xpt, range xrg, scalar xscal): the per-(range, key) and per-range B terms.
 struct MsmTerms {
   uint32_t n, rsize, npoint, nx;
-  uint32_t psize, nparts;         // batch split into nparts parts of psize terms (psize 0: one part)
+  uint32_t nparts;                // batch split into nparts interleaved parts (nparts <= 1: one part)
   const uint32_t* scal;
   const uint32_t* xpt;
   const uint32_t* xrg;

@@ -7,8 +7,8 @@
 // 128-bit z_i use the low windows only, full-width coefficients (B, keys) every window. Digits
 // are binned by (range, window, slice of 256 buckets) by a count / scan / scatter pass
 // (LDS-aggregated histograms, no global sort); each bin's workgroup counting-sorts its entries,
-// accumulates its buckets with 7M mixed additions (segmented lanes, LDS-DMA row gathers) and
-// reduces them to (sum_t (t+1) S_t, sum_t S_t). Windows with several slices combine them; a
+// accumulates its buckets with 7M mixed additions (segmented lanes, LDS-DMA row gathers); a
+// lane-parallel pass reduces each bin to (sum_t (t+1) S_t, sum_t S_t). Windows with several slices combine them; a
 // Horner pass per range joins the windows, multiplies by the cofactor and tests the identity
 // (src/batch.rs:212-216). Ranges > 1 only in the grouped fallback: independent MSMs over
 // contiguous slices of the signatures, one verdict each.
@@ -29,7 +29,7 @@ __device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t
   const uint32_t* src;
   if (!T.rsize) {
     pt = t;
-    rg = T.psize ? min(t / T.psize, T.nparts - 1) : 0;
+    rg = T.nparts > 1 ? t % T.nparts : 0;   // interleaved: every part gets its share of R, keys and B
     shrt = t >= 1 && t <= T.n;
     src = T.scal + (size_t)t * 8;
   } else if (t < T.npoint) {       // R_i (t < n), then one key term per signature
@@ -49,17 +49,21 @@ __device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t
   s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
 }
 
-// digits of term t: calls f(bin, local bucket, negative) for every non-zero digit
+// digits of term t: calls f(bin, local bucket, negative) for every non-zero digit. A term's top
+// window is unsigned (nothing sits above it: bit 128 for a z_i, bit 253 for a coefficient < l);
+// slice s of window w is split into nsub[w] sub-bins by term index.
 template <typename F>
-__device__ __forceinline__ void term_digits(const MsmPlan& P, bool shrt, uint32_t rg, const uint32_t s[8], F&& f) {
+__device__ __forceinline__ void term_digits(const MsmPlan& P, uint32_t t, bool shrt, uint32_t rg, const uint32_t s[8],
+                                            F&& f) {
   const uint32_t nw = shrt ? P.nwin_short : P.nwin;
   const uint32_t rbase = rg * P.bins_per_range;
   int carry = 0;
   for (uint32_t w = 0; w < nw; ++w) {
-    const int d = plan_digit(s, P.off[w], P.bits[w], carry, shrt && w + 1 == nw);
+    const int d = plan_digit(s, P.off[w], P.bits[w], carry, w + 1 == nw);
     if (d) {
       const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-      f(rbase + P.bin0[w] + (b >> SLICE_BITS), b & (NSLICE - 1), d < 0);
+      const uint32_t ns = P.nsub[w];
+      f(rbase + P.bin0[w] + (b >> SLICE_BITS) * ns + (t & (ns - 1)), b & (NSLICE - 1), d < 0);
     }
   }
 }
@@ -78,7 +82,7 @@ __global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32
     uint32_t pt, rg, s[8];
     bool shrt;
     term_get(T, t, pt, rg, shrt, s);
-    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
+    term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x)
@@ -129,7 +133,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     uint32_t pt, rg, s[8];
     bool shrt;
     term_get(T, t, pt, rg, shrt, s);
-    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
+    term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) {
@@ -144,7 +148,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     uint32_t pt, rg, s[8];
     bool shrt;
     term_get(T, t, pt, rg, shrt, s);
-    term_digits(P, shrt, rg, s, [&](uint32_t bin, uint32_t local, bool neg) {
+    term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t local, bool neg) {
       const uint32_t r = atomicAdd(&hist[bin], 1u);
       entries[gbase[bin] + r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local);
     });
@@ -260,6 +264,15 @@ __device__ __forceinline__ ge_niels ld_row_lds(const uint32_t* p) {
 // ends inside the lane's range is stored whole; the partial of a bucket that began before the
 // range ("head") goes to the lane's scratch slot; the lane holding a bucket's first entry adds the
 // heads of the following lanes the bucket covers after a barrier and stores the bucket.
+// Diagnostic build only (make variant VARIANT=stamps VFLAGS=-DEDC_STAMPS, tools/accum_stamps.py):
+// per-workgroup shader-clock stamps of the accumulation's phases; results are unchanged.
+#ifdef EDC_STAMPS
+__device__ unsigned long long g_acc_stamps[MSM_MAX_BINS * 8];
+#define ACC_STAMP(k, v) do { if (threadIdx.x == 0) g_acc_stamps[(size_t)blockIdx.x * 8 + (k)] = (v); } while (0)
+#else
+#define ACC_STAMP(k, v) do { } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin, uint32_t b) {
   return buckets + ((size_t)bin * NSLICE + b) * EXT_WORDS;
 }
@@ -276,13 +289,14 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
   __shared__ uint32_t lcnt[NSLICE];
   __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
   __shared__ uint32_t lcur[NSLICE];
-  // row buffers of the 4 waves during accumulation, then the 256 bucket sums for the reduction
-  __shared__ __attribute__((aligned(16))) uint32_t lbuf[NSLICE * EXT_WORDS];
-  static_assert(4 * WAVE_ROWS_WORDS <= NSLICE * EXT_WORDS, "row buffers fit the bucket image");
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS];   // row buffers of the 4 waves
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
+  ACC_STAMP(0, __builtin_amdgcn_s_memtime());
+  ACC_STAMP(5, __builtin_amdgcn_s_memrealtime());
+  ACC_STAMP(7, E);
   if (E == 0) {
     if (t == 0) {
       st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
@@ -329,6 +343,7 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
       if (en[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[en[u].y], 1u)] = en[u].x;
   }
   __syncthreads();   // workgroup-scope release/acquire: the sorted lists are read back below
+  ACC_STAMP(1, __builtin_amdgcn_s_memtime());
   const uint32_t lo = (uint32_t)(((uint64_t)E * t) >> 8), hi = (uint32_t)(((uint64_t)E * (t + 1)) >> 8);
   // bucket holding position lo: the first b with lend[b] > lo
   uint32_t cb = 0;
@@ -387,6 +402,7 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
       acc = ge_madd(acc, q);
     }
   }
+  ACC_STAMP(2, __builtin_amdgcn_s_memtime());
   // the open segment: a head partial, a whole bucket ending at hi, or the first part of a bucket
   // that continues into the next lanes
   const bool owns_open = lo < hi && !in_head;
@@ -402,19 +418,72 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
     }
     st_ext(bucket_slot(buckets, bin, cb), acc);
   }
-  // the bin's reduction (fused: its latency-bound steps overlap the other workgroups of the CU)
-  // W = sum_t (t+1) S_t and T = sum_t S_t over the 256 bucket sums (quad-cooperative)
-  __syncthreads();   // every bucket of the bin is stored
-  st_ext(lbuf + t * EXT_WORDS, ld_ext(bucket_slot(buckets, bin, t)));
-  __syncthreads();
-  ge_p3 ws, tot;
-  weighted_sum_256(lbuf, lbuf, lbuf + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
-  if (t < 4) {
-    ge_p3 W = quad_add(ws, tot);       // sum_t (t+1) S_t = sum_t t S_t + sum_t S_t
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+  ACC_STAMP(3, __builtin_amdgcn_s_memtime());
+  ACC_STAMP(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// ---- bin reduction: W = sum_t (t+1) S_t and T = sum_t S_t over a bin's 256 bucket sums ----
+// Lane-parallel (every lane adds its own points; quad-cooperative arithmetic would spend a whole
+// wave-instruction on 16 additions instead of 64): RED_LANES lanes per bin, RED_CHUNK = 256 /
+// RED_LANES consecutive buckets per lane, 64 / RED_LANES bins per wave. Lane j runs the chunk's
+// running sums from the top bucket down (s_j = sum_i B_i, r_j = sum_i (i+1) B_i), then the lanes
+// of a bin combine through shuffles: sum_t (t+1) B_t = sum_j r_j + RED_CHUNK * sum_{j>=1} Suf_j with
+// Suf_j = sum_{k>=j} s_k (a suffix scan), and T = Suf_0.
+#ifndef EDC_RED_LANES
+#define EDC_RED_LANES 32
+#endif
+constexpr int RED_LANES = EDC_RED_LANES;
+constexpr int RED_CHUNK = NSLICE / RED_LANES;
+constexpr int RED_BINS_PER_WG = 256 / RED_LANES;
+
+__device__ __forceinline__ fe shfl_down_fe(const fe& a, int d) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)__shfl_down((int)a.v[i], d, RED_LANES);
+  return r;
+}
+__device__ __forceinline__ ge_p3 shfl_down_pt(const ge_p3& P, int d) {
+  return ge_p3{shfl_down_fe(P.X, d), shfl_down_fe(P.Y, d), shfl_down_fe(P.Z, d), shfl_down_fe(P.T, d)};
+}
+
+__global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_t* __restrict__ counts,
+                                                    const uint32_t* __restrict__ buckets,
+                                                    uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
+  const uint32_t bin = blockIdx.x * RED_BINS_PER_WG + threadIdx.x / RED_LANES;
+  const int j = (int)(threadIdx.x % RED_LANES);
+  const bool live = bin < nbin && counts[bin] != 0;     // empty bins: the accumulation wrote W = T = 0
+  ge_p3 run = ge_identity(), acc = ge_identity();
+  if (live) {
+    const uint32_t* base = buckets + ((size_t)bin * NSLICE + (size_t)j * RED_CHUNK) * EXT_WORDS;
+    ge_p3 nxt = ld_ext(base + (RED_CHUNK - 1) * EXT_WORDS);
+    run = nxt;
+    acc = nxt;
+    for (int i = RED_CHUNK - 2; i >= 0; --i) {
+      const ge_p3 cur = ld_ext(base + i * EXT_WORDS);
+      run = ge_add(run, cur);
+      acc = ge_add(acc, run);
     }
+  }
+  // suffix scan of s_j = run over the bin's lanes (all lanes of a wave take part in the shuffles)
+  ge_p3 suf = run;
+  for (int d = 1; d < RED_LANES; d <<= 1) {
+    const ge_p3 o = shfl_down_pt(suf, d);
+    if (j + d < RED_LANES) suf = ge_add(suf, o);
+  }
+  // x_j = r_j + RED_CHUNK * Suf_j (j >= 1), x_0 = r_0; then the sum over the bin's lanes
+  ge_p3 x = acc;
+  if (j >= 1) {
+    ge_p3 y = suf;
+    for (int k = 1; k < RED_CHUNK; k <<= 1) y = ge_dbl(y);
+    x = ge_add(x, y);
+  }
+  for (int d = RED_LANES / 2; d >= 1; d >>= 1) {
+    const ge_p3 o = shfl_down_pt(x, d);
+    if (j < d) x = ge_add(x, o);
+  }
+  if (live && j == 0) {
+    st_ext(slice_W + (size_t)bin * EXT_WORDS, x);
+    st_ext(slice_T + (size_t)bin * EXT_WORDS, suf);
   }
 }
 
@@ -425,21 +494,20 @@ __global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* _
                                                     const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t g = blockIdx.x / P.nwin, w = blockIdx.x % P.nwin;
-  const uint32_t ns = P.nslice[w];
-  if (ns <= 1 && !P.sum_ranges) return;
+  const uint32_t ns = P.nslice[w], nsub = P.nsub[w];
+  if (ns * nsub <= 1 && !P.sum_ranges) return;
   __builtin_amdgcn_s_setprio(3);   // latency-bound tail: issue ahead of co-resident bulk waves
   const int t = threadIdx.x;
   const uint32_t b0 = g * P.bins_per_range + P.bin0[w];
-  // slice t's sums; parts of one batch (sum_ranges) are added first
+  // slice t's sums: its sub-bins, and the parts of one batch (sum_ranges), are added first
   ge_p3 sT = ge_identity(), sW = ge_identity();
   if ((uint32_t)t < ns) {
-    sT = ld_ext(slice_T + (size_t)(b0 + t) * EXT_WORDS);
-    sW = ld_ext(slice_W + (size_t)(b0 + t) * EXT_WORDS);
-    if (P.sum_ranges)
-      for (uint32_t p = 1; p < P.nranges; ++p) {
-        const size_t b = (size_t)p * P.bins_per_range + P.bin0[w] + t;
-        sT = ge_add(sT, ld_ext(slice_T + b * EXT_WORDS));
-        sW = ge_add(sW, ld_ext(slice_W + b * EXT_WORDS));
+    const uint32_t np = P.sum_ranges ? P.nranges : 1u;
+    for (uint32_t p = 0; p < np; ++p)
+      for (uint32_t u = 0; u < nsub; ++u) {
+        const size_t b = (P.sum_ranges ? (size_t)p * P.bins_per_range + P.bin0[w] : b0) + (size_t)t * nsub + u;
+        const ge_p3 T = ld_ext(slice_T + b * EXT_WORDS), W = ld_ext(slice_W + b * EXT_WORDS);
+        if (p == 0 && u == 0) { sT = T; sW = W; } else { sT = ge_add(sT, T); sW = ge_add(sW, W); }
       }
   }
   uint32_t* lpts = smem;
@@ -509,7 +577,7 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
 // window sum of (range g, window w): combined by k_msm_window, or the single bin's W
 __device__ __forceinline__ ge_p3 window_sum(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* slice_W,
                                              const uint32_t* win) {
-  if (P.nslice[w] > 1 || P.sum_ranges) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
+  if (P.nslice[w] * P.nsub[w] > 1 || P.sum_ranges) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
   return ld_ext(slice_W + (size_t)(g * P.bins_per_range + P.bin0[w]) * EXT_WORDS);
 }
 
@@ -589,16 +657,25 @@ static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t); 
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
                        uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
-  // one workgroup per bin; the bin reduction is fused into the accumulation
+  // one workgroup per bin, then the lane-parallel bin reductions
   hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
                      heads, slice_W, slice_T);
+  hipLaunchKernelGGL(k_msm_reduce, dim3(cdiv(P.nbin(), RED_BINS_PER_WG)), dim3(256), 0, st, P.nbin(), counts, buckets,
+                     slice_W, slice_T);
 }
+
+#ifdef EDC_STAMPS
+extern "C" int edc_debug_acc_stamps(void* out, size_t bytes) {
+  if (bytes > sizeof(g_acc_stamps)) bytes = sizeof(g_acc_stamps);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_acc_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t msm_bucket_words(uint32_t nbin) { return (size_t)nbin * NSLICE * EXT_WORDS; }
 
 static bool plan_multi(const MsmPlan& P) {
   for (uint32_t w = 0; w < P.nwin; ++w)
-    if (P.nslice[w] > 1) return true;
+    if (P.nslice[w] * P.nsub[w] > 1) return true;
   return false;
 }
 

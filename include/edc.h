@@ -257,6 +257,13 @@ int edc_set_key_grouping(edc_ctx* ctx, int mode);
 int edc_set_msm_shape(edc_ctx* ctx, int bits, int parts);
 
 /*
+ * Target MSM entries per bin (tuning / measurement; >= 256, 0 = from the batch size, default):
+ * with automatic parts, the slices of the densest windows are split into sub-bins of about this
+ * many digits each, one workgroup per bin. Results never depend on it.
+ */
+int edc_set_msm_bin_entries(edc_ctx* ctx, int entries);
+
+/*
  * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous
  * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). Results never depend
  * on it.

@@ -42,6 +42,21 @@ void hc_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   words_to_bytes(wo, out);
 }
 
+// raw limbs in (any lazy form the caller picks, e.g. every limb at the mul-input bound):
+// op 0 mul, 1 sqr; out = canonical bytes, lim = the output limbs
+void hc_fe_limbs(int op, const uint32_t* a, const uint32_t* b, uint8_t* out, uint32_t* lim) {
+  fe x, y, r;
+  for (int i = 0; i < 9; ++i) { x.v[i] = a[i]; y.v[i] = b[i]; }
+  switch (op) {
+    case 0: r = fe_mul(x, y); break;
+    default: r = fe_sqr(x); break;
+  }
+  for (int i = 0; i < 9; ++i) lim[i] = r.v[i];
+  uint32_t wo[8];
+  fe_to_words(r, wo);
+  words_to_bytes(wo, out);
+}
+
 // stress the lazy bounds: r = ((a+b)*(c+d) - (a*b)) chained k times
 void hc_fe_chain(const uint8_t* a, const uint8_t* b, int k, uint8_t* out) {
   uint32_t wa[8], wb[8], wo[8];

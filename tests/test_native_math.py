@@ -63,6 +63,29 @@ def test_lazy_bound_chains(hc, oracle):
         assert int.from_bytes(out.raw, "little") == y % P
 
 
+def test_mul_at_input_bound(hc, oracle):
+    """fe_mul / fe_sqr on limbs at and near the mul-input bound (every limb up to twice the
+    reduced bound: a lazy sum of two reduced elements): the value mod p, and reduced outputs
+    (limbs < 2^29 + 2^19)."""
+    P = oracle.P
+    rnd = random.Random(29)
+    top = 2 * ((1 << 29) + (1 << 19)) - 1
+    LimbsT = ctypes.c_uint32 * 9
+    out = ctypes.create_string_buffer(32)
+    lim = LimbsT()
+    cases = [[top] * 9, [top] * 8 + [0], [0] * 8 + [top], [(1 << 29) - 1] * 9]
+    cases += [[rnd.randrange(top + 1) for _ in range(9)] for _ in range(300)]
+    cases += [[top - rnd.randrange(1 << 12) for _ in range(9)] for _ in range(100)]
+    for i, a in enumerate(cases):
+        b = cases[(i * 5 + 1) % len(cases)]
+        va = sum(x << (29 * k) for k, x in enumerate(a))
+        vb = sum(x << (29 * k) for k, x in enumerate(b))
+        for op, exp in [(0, va * vb), (1, va * va)]:
+            hc.hc_fe_limbs(op, LimbsT(*a), LimbsT(*b), out, lim)
+            assert int.from_bytes(out.raw, "little") == exp % P, (op, a, b)
+            assert max(lim) < (1 << 29) + (1 << 19), (op, list(lim))
+
+
 def test_decompress_and_point_ops(hc, oracle):
     from conftest import golden
     out = ctypes.create_string_buffer(64)
