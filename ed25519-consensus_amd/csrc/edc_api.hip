@@ -40,6 +40,7 @@ struct Slot {
   uint32_t *table = nullptr, *slot_key = nullptr;
   uint32_t *pts = nullptr, *scal = nullptr;
   unsigned long long *key_acc = nullptr, *u_acc = nullptr;
+  uint32_t* coef_part = nullptr;     // k_coef's per-workgroup key slots (merged by k_coef_merge)
   uint8_t *itembad = nullptr, *keybad = nullptr;   // per-item / per-key failure bits (fallback)
   // MSM workspace, grown on demand to the plan's bins / entries
   uint32_t cap_bins = 0, cap_ranges = 0;
@@ -144,11 +145,12 @@ static void free_msm_buffers(Slot& s) {
 
 static void free_slot_buffers(Slot& s) {
   void* ptrs[] = {s.k, s.key_slot, s.key_index, s.key_rep, s.table, s.slot_key, s.pts, s.scal, s.key_acc,
-                  s.u_acc, s.itembad, s.keybad};
+                  s.u_acc, s.itembad, s.keybad, s.coef_part};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s.k = s.key_slot = s.key_index = s.key_rep = s.table = s.slot_key = s.pts = s.scal = nullptr;
   s.key_acc = s.u_acc = nullptr;
+  s.coef_part = nullptr;
   s.itembad = s.keybad = nullptr;
   free_msm_buffers(s);
   s.cap_n = s.cap_T = 0;
@@ -201,6 +203,7 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.scal, (2 + 2 * cap) * 8));
   CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
   CK(dalloc(&s.u_acc, (cap / COEF_CHUNK + 2) * KEY_ACC_LIMBS));   // one sum per fallback range
+  CK(dalloc(&s.coef_part, coef_part_words(cap)));
   CK(dalloc(&s.itembad, cap));
   CK(dalloc(&s.keybad, cap));
   launch_init_basepoint(s.st, s.pts);
@@ -549,7 +552,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
-              per_sig);
+              per_sig, s.coef_part);
   mark(PH_MSM_BIN);
   if (with_bin) launch_msm_bin(st, *P, batch_terms(*P, s, N), 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries,
                               s.flags);

@@ -20,7 +20,9 @@ void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig);
+                 bool per_sig, uint32_t* coef_part);
+// words of k_coef's per-workgroup key-slot dump for batches of up to cap_n signatures
+size_t coef_part_words(size_t cap_n);
 // grouped fallback: per-(range, key) / per-range coefficients as listed MSM terms
 void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nranges, uint32_t m, bool per_sig,
                        const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],

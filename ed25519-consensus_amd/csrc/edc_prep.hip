@@ -204,6 +204,11 @@ struct seed8 { uint32_t w[8]; };
 constexpr int COEF_SIGS_PER_THREAD = 8;             // two ChaCha blocks -> z for 8 signatures
 constexpr int COEF_SLOTS = 256;                     // LDS key-accumulator slots
 constexpr int PL = 12;                              // limbs of a 128 x 256-bit product
+static_assert(PL == KEY_ACC_LIMBS, "limb sums");
+// k_coef's per-workgroup slot dump (batch mode): nwg x COEF_SLOTS tags, then the 64-bit sums
+__device__ __forceinline__ unsigned long long* coef_part_sums(uint32_t* part, uint32_t nwg) {
+  return reinterpret_cast<unsigned long long*>(part + (((size_t)nwg * COEF_SLOTS + 1) & ~(size_t)1));
+}
 static_assert(COEF_CHUNK == 256 * COEF_SIGS_PER_THREAD, "k_coef chunk (edc_common.h)");
 
 // r[0..11] = z (4 limbs) * s (8 limbs), exact
@@ -240,7 +245,8 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               unsigned long long* __restrict__ key_acc,
                                               unsigned long long* __restrict__ u_acc,
                                               uint8_t* __restrict__ itembad,
-                                              int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m) {
+                                              int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m,
+                                              uint32_t* __restrict__ coef_part) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
@@ -338,6 +344,21 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
     unsigned long long x = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     atomicAdd(&u_acc[(rsize ? (size_t)(base / rsize) * PL : 0) + threadIdx.x], x);
   }
+  if (coef_part) {
+    // batch mode: this workgroup's key slots go out as plain stores, merged per slot by
+    // k_coef_merge (a few validators' sums hit by every workgroup made the global atomics
+    // serialize: 0.09 of the 0.17 ms of this phase at 2^20 votes from 150 keys)
+    uint32_t* ptag = coef_part + (size_t)blockIdx.x * COEF_SLOTS;
+    unsigned long long* psum = coef_part_sums(coef_part, gridDim.x) + (size_t)blockIdx.x * COEF_SLOTS * PL;
+    for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
+      ptag[s] = tag[s];
+      if (tag[s] != 0xFFFFFFFFu) {
+#pragma unroll
+        for (int j = 0; j < PL; ++j) psum[(size_t)s * PL + j] = acc[s][j];
+      }
+    }
+    return;
+  }
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
     const uint32_t key = tag[s];
     if (key != 0xFFFFFFFFu) {
@@ -345,6 +366,54 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
       for (int j = 0; j < PL; ++j) atomicAdd(&key_acc[(size_t)key * PL + j], acc[s][j]);
     }
   }
+}
+
+// Per LDS slot s: the sums the k_coef workgroups left for s. The slot's usual key (the first
+// non-empty tag seen) is summed in registers and added once; other keys sharing the slot (more
+// than COEF_SLOTS distinct keys) go to key_acc by atomics, which are then rarely contended.
+__global__ void __launch_bounds__(256) k_coef_merge(uint32_t nwg, const uint32_t* __restrict__ coef_part,
+                                                    unsigned long long* __restrict__ key_acc) {
+  __shared__ uint32_t lead;
+  __shared__ unsigned long long red[4][PL];
+  const uint32_t s = blockIdx.x, t = threadIdx.x;
+  const unsigned long long* psum = coef_part_sums(const_cast<uint32_t*>(coef_part), nwg);
+  if (t == 0) lead = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t w = t; w < nwg; w += blockDim.x) {
+    const uint32_t tg = coef_part[(size_t)w * COEF_SLOTS + s];
+    if (tg != 0xFFFFFFFFu) atomicCAS(&lead, 0xFFFFFFFFu, tg);
+  }
+  __syncthreads();
+  const uint32_t L = lead;
+  if (L == 0xFFFFFFFFu) return;                 // uniform: no workgroup used this slot
+  unsigned long long mine[PL];
+#pragma unroll
+  for (int j = 0; j < PL; ++j) mine[j] = 0;
+  for (uint32_t w = t; w < nwg; w += blockDim.x) {
+    const uint32_t tg = coef_part[(size_t)w * COEF_SLOTS + s];
+    if (tg == 0xFFFFFFFFu) continue;
+    const unsigned long long* src = psum + ((size_t)w * COEF_SLOTS + s) * PL;
+    if (tg == L) {
+#pragma unroll
+      for (int j = 0; j < PL; ++j) mine[j] += src[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < PL; ++j) atomicAdd(&key_acc[(size_t)tg * PL + j], src[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PL; ++j) {
+    unsigned long long x = mine[j];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_down(x, d, 64);
+    mine[j] = x;
+  }
+  if ((t & 63) == 0) {
+#pragma unroll
+    for (int j = 0; j < PL; ++j) red[t >> 6][j] = mine[j];
+  }
+  __syncthreads();
+  if (t < PL) atomicAdd(&key_acc[(size_t)L * PL + t], red[0][t] + red[1][t] + red[2][t] + red[3][t]);
 }
 
 // sum_j L[j] * 2^(32 j) mod l for PL limb sums L[j] < 2^64 (value < 2^448)
@@ -451,15 +520,24 @@ void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags) {
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig) {
+                 bool per_sig, uint32_t* coef_part) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
-  if (n)
-    hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
-                       key_index, scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u);
+  if (n) {
+    const uint32_t nwg = cdiv(n, COEF_CHUNK);
+    uint32_t* part = per_sig ? nullptr : coef_part;
+    hipLaunchKernelGGL(k_coef, dim3(nwg), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index, scal, key_acc,
+                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part);
+    if (part) hipLaunchKernelGGL(k_coef_merge, dim3(COEF_SLOTS), dim3(256), 0, st, nwg, part, key_acc);
+  }
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
                      u_acc, scal, flags, per_sig ? 1 : 0);
 }
+size_t coef_part_words(size_t cap_n) {
+  const size_t nwg = (cap_n + COEF_CHUNK - 1) / COEF_CHUNK;
+  return ((nwg * COEF_SLOTS + 1) & ~(size_t)1) + nwg * COEF_SLOTS * PL * 2;
+}
+
 void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nranges, uint32_t m, bool per_sig,
                        const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],
                        uint64_t zbase, const uint32_t* key_index, uint32_t* scal, unsigned long long* key_acc,
@@ -471,7 +549,8 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   (void)hipMemsetAsync(u_acc, 0, (size_t)nranges * PL * sizeof(unsigned long long), st);
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
-                       key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm);
+                       key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm,
+                       (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }
