@@ -132,16 +132,11 @@ __device__ __forceinline__ uint32_t key_hash(const uint32_t w[8], uint32_t s0, u
 // Open-addressing insert keyed by the raw 32 key bytes. table[] holds the index of the first
 // signature that claimed the slot (0xFFFFFFFF = empty; a slot never changes once claimed, so a
 // stale relaxed read is safe). The claimer also draws the dense key index.
-__global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* __restrict__ vk,
-                                                    uint32_t* __restrict__ table, uint32_t tmask,
-                                                    uint32_t salt0, uint32_t salt1, uint32_t probe_cap,
-                                                    uint32_t* __restrict__ slot_key,
-                                                    uint32_t* __restrict__ key_slot_of_sig,
-                                                    uint32_t* __restrict__ key_rep,
-                                                    unsigned long long* __restrict__ key_acc,
-                                                    int* __restrict__ flags) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void key_insert_one(uint32_t i, const uint8_t* __restrict__ vk,
+                                               uint32_t* __restrict__ table, uint32_t tmask, uint32_t salt0,
+                                               uint32_t salt1, uint32_t probe_cap, uint32_t* __restrict__ slot_key,
+                                               uint32_t* __restrict__ key_slot_of_sig, uint32_t* __restrict__ key_rep,
+                                               unsigned long long* __restrict__ key_acc, int* __restrict__ flags) {
   uint32_t w[8];
   ld_words8(vk + (size_t)i * 32, w);
   uint32_t h = key_hash(w, salt0, salt1) & tmask;
@@ -183,6 +178,37 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
     h = (h + 1) & tmask;
   }
   atomicOr(&flags[FLAG_OVF], 1);    // give up grouping for this batch (see KEY_PROBE_CAP)
+}
+
+__global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* __restrict__ vk,
+                                                    uint32_t* __restrict__ table, uint32_t tmask,
+                                                    uint32_t salt0, uint32_t salt1, uint32_t probe_cap,
+                                                    uint32_t* __restrict__ slot_key,
+                                                    uint32_t* __restrict__ key_slot_of_sig,
+                                                    uint32_t* __restrict__ key_rep,
+                                                    unsigned long long* __restrict__ key_acc,
+                                                    int* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) key_insert_one(i, vk, table, tmask, salt0, salt1, probe_cap, slot_key, key_slot_of_sig, key_rep,
+                            key_acc, flags);
+}
+
+// Seeding pass over a sample of KEY_SEED_SAMPLE signatures (multiplicative hashing of the sample
+// index, so that no period in the key order -- e.g. round-robin validators -- aliases): the table is empty
+// at the start of a batch, and without it every concurrently resident lane of k_key_insert sees
+// its validator's slot still empty and CASes it -- a million CAS on ~150 words, serialized in
+// L2 (0.1 ms at 2^20). With the validators claimed here, the full pass finds them with plain loads.
+constexpr uint32_t KEY_SEED_SAMPLE = 4096;
+__global__ void __launch_bounds__(256) k_key_seed(uint32_t n, const uint8_t* __restrict__ vk,
+                                                  uint32_t* __restrict__ table, uint32_t tmask,
+                                                  uint32_t salt0, uint32_t salt1, uint32_t probe_cap,
+                                                  uint32_t* __restrict__ slot_key,
+                                                  uint32_t* __restrict__ key_slot_of_sig,
+                                                  uint32_t* __restrict__ key_rep,
+                                                  unsigned long long* __restrict__ key_acc,
+                                                  int* __restrict__ flags) {
+  const uint32_t i = (uint32_t)(((uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u) % n);
+  key_insert_one(i, vk, table, tmask, salt0, salt1, probe_cap, slot_key, key_slot_of_sig, key_rep, key_acc, flags);
 }
 
 // dense key index per signature; after a probe overflow the batch falls back to one key term
@@ -508,8 +534,12 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
                  uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags) {
   if (!n) return;
-  hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt[0], salt[1],
-                     force_overflow ? 0u : KEY_PROBE_CAP,
+  const uint32_t cap = force_overflow ? 0u : KEY_PROBE_CAP;
+  if (n > 4 * KEY_SEED_SAMPLE) {
+    hipLaunchKernelGGL(k_key_seed, dim3(KEY_SEED_SAMPLE / 256), dim3(256), 0, st, n, vk, table, tmask,
+                       salt[0], salt[1], cap, slot_key, key_slot_of_sig, key_rep, key_acc, flags);
+  }
+  hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt[0], salt[1], cap,
                      slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index, flags);
