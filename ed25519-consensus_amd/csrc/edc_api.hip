@@ -51,6 +51,7 @@ struct Slot {
   uint32_t *slice_W = nullptr, *slice_T = nullptr, *win = nullptr;
   uint32_t* buckets = nullptr;  // bins x 256 bucket sums (extended)
   uint32_t* heads = nullptr;    // bins x 256 head partials of the segmented accumulation
+  uint32_t* bucket_end = nullptr;   // bins x 256 bucket end positions of the sorted entries
   int* flags = nullptr;
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
@@ -134,10 +135,12 @@ struct edc_ctx {
   } while (0)
 
 static void free_msm_buffers(Slot& s) {
-  void* ptrs[] = {s.counts, s.offsets, s.cursor, s.slice_W, s.slice_T, s.win, s.buckets, s.heads, s.entries, s.sorted};
+  void* ptrs[] = {s.counts, s.offsets, s.cursor, s.slice_W, s.slice_T, s.win, s.buckets, s.heads, s.entries, s.sorted,
+                  s.bucket_end};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s.counts = s.offsets = s.cursor = s.slice_W = s.slice_T = s.win = s.buckets = s.heads = s.sorted = nullptr;
+  s.bucket_end = nullptr;
   s.entries = nullptr;
   s.cap_bins = s.cap_ranges = 0;
   s.cap_entries = 0;
@@ -220,11 +223,12 @@ static int ensure_msm(edc_ctx* ctx, Slot& s, const MsmPlan& P, size_t entries) {
   if (nbin > s.cap_bins || P.nranges > s.cap_ranges) {
     CK(hipStreamSynchronize(s.st));
     for (void* p : {(void*)s.counts, (void*)s.offsets, (void*)s.cursor, (void*)s.slice_W, (void*)s.slice_T,
-                    (void*)s.win, (void*)s.buckets, (void*)s.heads})
+                    (void*)s.win, (void*)s.buckets, (void*)s.heads, (void*)s.bucket_end})
       if (p) (void)hipFree(p);
     const uint32_t nb = nbin > s.cap_bins ? nbin : s.cap_bins;
     const uint32_t nr = P.nranges > s.cap_ranges ? P.nranges : (s.cap_ranges ? s.cap_ranges : 1);
     s.counts = s.offsets = s.cursor = s.slice_W = s.slice_T = s.win = s.buckets = s.heads = nullptr;
+    s.bucket_end = nullptr;
     s.cap_bins = s.cap_ranges = 0;
     CK(dalloc(&s.counts, nb));
     CK(dalloc(&s.offsets, nb));
@@ -234,6 +238,7 @@ static int ensure_msm(edc_ctx* ctx, Slot& s, const MsmPlan& P, size_t entries) {
     CK(dalloc(&s.win, (size_t)nr * MSM_MAX_WIN * EXT_WORDS));
     CK(dalloc(&s.buckets, msm_bucket_words(nb)));
     CK(dalloc(&s.heads, msm_bucket_words(nb)));
+    CK(dalloc(&s.bucket_end, (size_t)nb * NSLICE));
     s.cap_bins = nb;
     s.cap_ranges = nr;
   }
@@ -578,7 +583,8 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   if (rc) return rc;
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
-  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
+  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
+                    s.slice_T);
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
   launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
   if (s.timed) (void)hipEventRecord(s.ev[PH_N], st);
@@ -1004,7 +1010,8 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
                        ctx->fb_xscal};
   launch_msm_bin(st, P, terms, npoint + (uint32_t)nx, s.counts, s.offsets, s.cursor, s.entries, s.flags);
-  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.pts, s.buckets, s.heads, s.slice_W, s.slice_T);
+  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
+                    s.slice_T);
   launch_msm_range_tail(st, P, s.slice_W, s.slice_T, s.win, ctx->fb_rv);
   CK(hipMemsetAsync(ctx->fb_rv + G, 0, G, st));
   launch_range_prebad(st, (uint32_t)n, (uint32_t)rsize, s.itembad, s.keybad, s.key_index, per_sig, ctx->fb_rv + G);

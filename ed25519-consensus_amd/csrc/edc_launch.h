@@ -40,8 +40,8 @@ void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, con
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
-                       uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T);
+                       const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
+                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T);
 size_t msm_bucket_words(uint32_t nbin);
 void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out);

@@ -277,37 +277,25 @@ __device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin
   return buckets + ((size_t)bin * NSLICE + b) * EXT_WORDS;
 }
 
-__global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __restrict__ counts,
-                                                                   const uint32_t* __restrict__ offsets,
-                                                                   const uint2* __restrict__ entries,
-                                                                   uint32_t* __restrict__ sorted,
-                                                                   const uint32_t* __restrict__ pts,
-                                                                   uint32_t* __restrict__ buckets,
-                                                                   uint32_t* __restrict__ heads,
-                                                                   uint32_t* __restrict__ slice_W,
-                                                                   uint32_t* __restrict__ slice_T) {
+// Counting sort of each bin's entries by bucket (one workgroup per bin): sorted[] gets the point
+// indices (sign in bit 31) bucket by bucket, bucket_end[] the exclusive end position of every
+// bucket, and empty buckets get the identity. A kernel of its own, so the memory-bound sort of one
+// batch overlaps the VALU-bound accumulation of another instead of idling the accumulation's CUs
+// (every workgroup of a launch sorts at the same time).
+__global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ counts,
+                                                  const uint32_t* __restrict__ offsets,
+                                                  const uint2* __restrict__ entries, uint32_t* __restrict__ sorted,
+                                                  uint32_t* __restrict__ bucket_end, uint32_t* __restrict__ buckets) {
   __shared__ uint32_t lcnt[NSLICE];
-  __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
   __shared__ uint32_t lcur[NSLICE];
-  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS];   // row buffers of the 4 waves
   const int t = threadIdx.x;
-  const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;
   const uint32_t E = counts[bin];
-  ACC_STAMP(0, __builtin_amdgcn_s_memtime());
-  ACC_STAMP(5, __builtin_amdgcn_s_memrealtime());
-  ACC_STAMP(7, E);
-  if (E == 0) {
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
-    }
-    return;
-  }
+  if (E == 0) return;
   const uint32_t off = offsets[bin];
   lcnt[t] = 0;
   __syncthreads();
-  // counting sort by bucket; loads are batched 8 deep so the passes are not latency-bound
+  // loads are batched 8 deep so the passes are not latency-bound
   constexpr int SB = 8;
   for (uint32_t e0 = t; e0 < E; e0 += 256 * SB) {
     uint32_t y[SB];
@@ -329,8 +317,9 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
       if (t >= d) incl += v;
     }
     uint32_t run = incl - sum;
+    uint32_t* be = bucket_end + (size_t)bin * NSLICE + 4 * t;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { lcur[4 * t + q] = run; run += c[q]; lend[4 * t + q] = run; }
+    for (int q = 0; q < 4; ++q) { lcur[4 * t + q] = run; run += c[q]; be[q] = run; }
   }
   __syncthreads();
   if (lcnt[t] == 0) st_ext(bucket_slot(buckets, bin, t), ge_identity());
@@ -342,7 +331,36 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
     for (int u = 0; u < SB; ++u)
       if (en[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[en[u].y], 1u)] = en[u].x;
   }
-  __syncthreads();   // workgroup-scope release/acquire: the sorted lists are read back below
+}
+
+__global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __restrict__ counts,
+                                                                   const uint32_t* __restrict__ offsets,
+                                                                   const uint32_t* __restrict__ sorted,
+                                                                   const uint32_t* __restrict__ bucket_end,
+                                                                   const uint32_t* __restrict__ pts,
+                                                                   uint32_t* __restrict__ buckets,
+                                                                   uint32_t* __restrict__ heads,
+                                                                   uint32_t* __restrict__ slice_W,
+                                                                   uint32_t* __restrict__ slice_T) {
+  __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS];   // row buffers of the 4 waves
+  const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
+  const uint32_t bin = blockIdx.x;
+  const uint32_t E = counts[bin];
+  ACC_STAMP(0, __builtin_amdgcn_s_memtime());
+  ACC_STAMP(5, __builtin_amdgcn_s_memrealtime());
+  ACC_STAMP(7, E);
+  if (E == 0) {
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, ge_identity());
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, ge_identity());
+    }
+    return;
+  }
+  const uint32_t off = offsets[bin];
+  lend[t] = bucket_end[(size_t)bin * NSLICE + t];
+  __syncthreads();
   ACC_STAMP(1, __builtin_amdgcn_s_memtime());
   const uint32_t lo = (uint32_t)(((uint64_t)E * t) >> 8), hi = (uint32_t)(((uint64_t)E * (t + 1)) >> 8);
   // bucket holding position lo: the first b with lend[b] > lo
@@ -351,7 +369,7 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
   for (int step = 128; step >= 1; step >>= 1)
     if (lend[cb + step - 1] <= lo) cb += step;
   cb = min(cb, (uint32_t)NSLICE - 1);              // lanes with an empty range (E < 256)
-  const bool head0 = lo < hi && lend[cb] - lcnt[cb] < lo;   // first bucket began in an earlier lane
+  const bool head0 = lo < hi && (cb ? lend[cb - 1] : 0u) < lo;   // first bucket began in an earlier lane
   bool in_head = head0;
   uint32_t cend = lend[cb];
   const uint32_t rounds = __builtin_amdgcn_readfirstlane(((uint64_t)E + 255) >> 8);
@@ -655,11 +673,13 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
 
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
-                       const uint2* entries, uint32_t* sorted, const uint32_t* pts, uint32_t* buckets,
-                       uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
-  // one workgroup per bin, then the lane-parallel bin reductions
-  hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, pts, buckets,
-                     heads, slice_W, slice_T);
+                       const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
+                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
+  // one workgroup per bin (sort, then accumulation), then the lane-parallel bin reductions
+  hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end,
+                     buckets);
+  hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
+                     buckets, heads, slice_W, slice_T);
   hipLaunchKernelGGL(k_msm_reduce, dim3(cdiv(P.nbin(), RED_BINS_PER_WG)), dim3(256), 0, st, P.nbin(), counts, buckets,
                      slice_W, slice_T);
 }
