@@ -45,7 +45,7 @@ __device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t
     src = T.xscal + (size_t)q * 8;
   }
   const uint4* q4 = reinterpret_cast<const uint4*>(src);
-  const uint4 a = q4[0], b = q4[1];
+  const uint4 a = q4[0], b = shrt ? make_uint4(0u, 0u, 0u, 0u) : q4[1];   // a z_i is 128 bits
   s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w; s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
 }
 
@@ -416,8 +416,7 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
     e = e_next;
     if (pos + 2 < hi) e_next = sorted[off + pos + 2];
     if (pos < hi) {
-      if (e_cur >> 31) q = ge_niels_neg(q);
-      acc = ge_madd(acc, q);
+      acc = ge_madd_sgn(acc, q, (e_cur >> 31) != 0);
     }
   }
   ACC_STAMP(2, __builtin_amdgcn_s_memtime());

@@ -108,8 +108,7 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
     int b = radix16_digit(s, sc, j);
     int bi = b < 0 ? -b : b;
     ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
-    if (b < 0) nb = ge_niels_neg(nb);
-    acc = ge_madd(acc, nb);
+    acc = ge_madd_sgn(acc, nb, b < 0);
   }
   return acc;
 }
@@ -126,14 +125,12 @@ __device__ ge_p3 comb_double_base(const uint32_t k[8], const uint32_t s[8], cons
     const int a = radix16_digit(k, kc, j);
     const int ai = a < 0 ? -a : a;
     ge_niels q = ai ? ld_niels(acomb, j * COMB_MULT + ai - 1) : ge_niels_identity();
-    if (a > 0) q = ge_niels_neg(q);            // -[k]A
-    acc = ge_madd(acc, q);
+    acc = ge_madd_sgn(acc, q, a > 0);          // -[k]A
     EDC_SCHED_FENCE();
     const int b = radix16_digit(s, sc, j);
     const int bi = b < 0 ? -b : b;
     ge_niels nb = bi ? ld_niels(bcomb, j * COMB_MULT + bi - 1) : ge_niels_identity();
-    if (b < 0) nb = ge_niels_neg(nb);
-    acc = ge_madd(acc, nb);
+    acc = ge_madd_sgn(acc, nb, b < 0);
   }
   return acc;
 }
@@ -285,8 +282,7 @@ __device__ ge_p3 base_mul(const uint32_t x[8], const uint32_t* btab) {
     int b = d[j];
     int bi = b < 0 ? -b : b;
     ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
-    if (b < 0) nb = ge_niels_neg(nb);
-    acc = ge_madd(acc, nb);
+    acc = ge_madd_sgn(acc, nb, b < 0);
   }
   return acc;
 }

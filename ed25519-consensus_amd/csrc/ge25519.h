@@ -140,6 +140,32 @@ EDC_HD ge_p3 ge_add_cached(const ge_p3& P, const ge_cached& q) {
   return r;
 }
 
+// P + Q (neg = false) or P - Q (neg = true), Q affine Niels: 7M. -Q is (y-x, y+x, -2dxy), so
+// the sign only swaps which of Y-X, Y+X meets which record half, and F / G (C changes sign):
+// 36 selects instead of ge_niels_neg's swap, negation and select of the whole record.
+EDC_HD ge_p3 ge_madd_sgn(const ge_p3& P, const ge_niels& q, bool neg) {
+  const fe ym = fe_select(q.ymx, q.ypx, neg), yp = fe_select(q.ypx, q.ymx, neg);
+  fe A = fe_mul(fe_sub(P.Y, P.X), ym);
+  EDC_SCHED_FENCE();
+  fe B = fe_mul(fe_add(P.Y, P.X), yp);
+  EDC_SCHED_FENCE();
+  fe C = fe_mul(P.T, q.xy2d);
+  EDC_SCHED_FENCE();
+  fe D = fe_add_c(P.Z, P.Z);
+  fe E = fe_sub(B, A), H = fe_add(B, A);
+  const fe dmc = fe_sub(D, C), dpc = fe_add(D, C);
+  fe F = fe_select(dmc, dpc, neg), G = fe_select(dpc, dmc, neg);
+  ge_p3 r;
+  r.X = fe_mul(E, F);
+  EDC_SCHED_FENCE();
+  r.Y = fe_mul(G, H);
+  EDC_SCHED_FENCE();
+  r.T = fe_mul(E, H);
+  EDC_SCHED_FENCE();
+  r.Z = fe_mul(F, G);
+  return r;
+}
+
 // P + Q both extended: 9M
 EDC_HD ge_p3 ge_add(const ge_p3& P, const ge_p3& Q) { return ge_add_cached(P, ge_to_cached(Q)); }
 

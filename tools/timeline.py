@@ -46,6 +46,25 @@ def main():
           f"GPU busy {busy/span*100:.1f} %")
     for k in sorted(level):
         print(f"  concurrency {k}: {level[k]/span*100:.1f} %")
+    # what runs alone: time at concurrency 1 per kernel, and time when only latency-tail kernels
+    # (single-workgroup Horner / window combine) or runtime fills occupy the GPU
+    tail = ("k_msm_final", "k_msm_window", "k_msm_range_final", "__amd_rocclr")
+    ev2 = sorted([(s, 1, n) for s, e, n in sel] + [(e, -1, n) for s, e, n in sel], key=lambda x: (x[0], x[1]))
+    running = defaultdict(int)
+    solo = defaultdict(int)
+    tail_only = 0
+    last = t0
+    for t, d, n in ev2:
+        live = [k for k, c in running.items() if c > 0]
+        if len(live) == 1 and sum(running.values()) == 1:
+            solo[live[0]] += t - last
+        if live and all(any(x in k for x in tail) for k in live):
+            tail_only += t - last
+        running[n] += d
+        last = t
+    print(f"  only tail kernels / fills running: {tail_only/span*100:.1f} % of the span")
+    for n, v in sorted(solo.items(), key=lambda x: -x[1]):
+        print(f"  alone: {n:40s} {v/span*100:.1f} %")
     tot = sum(per.values())
     for n, v in sorted(per.items(), key=lambda x: -x[1]):
         print(f"  {n:40s} {v/1e6/a.batches:.3f} ms/batch (kernel-time {v/tot*100:.1f} %)")
