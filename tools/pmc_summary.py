@@ -17,17 +17,20 @@ MAD_CYC, OTHER_CYC, SIMDS = 4.46, 2.5, 1024     # profiles/r01_valu_rates.txt; 2
 
 
 def medians(path):
-    """{kernel short name: {counter: median over this kernel's dispatches with its largest grid}}
-    (the bench's batch-size launches; the small signing / setup launches have smaller grids)"""
+    """{kernel short name: {counter: median over this kernel's dispatches with its most frequent grid}}
+    (the bench's steady-state batch launches)"""
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"].split("(")[0].replace("edc::", "")
             if name in KERNELS:
                 rows.append((name, int(r["Grid_Size"]), r["Counter_Name"], float(r["Counter_Value"])))
-    top = {}
+    # the steady-state dispatches: the grid size seen most often per kernel (the first batch of a
+    # context runs without a key-ratio hint, so its MSM plan and grids differ)
+    seen = defaultdict(lambda: defaultdict(int))
     for name, g, _, _ in rows:
-        top[name] = max(top.get(name, 0), g)
+        seen[name][g] += 1
+    top = {name: max(gs.items(), key=lambda x: (x[1], x[0]))[0] for name, gs in seen.items()}
     per = defaultdict(lambda: defaultdict(list))
     for name, g, c, v in rows:
         if g == top[name]:
