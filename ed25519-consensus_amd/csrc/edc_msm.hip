@@ -441,41 +441,40 @@ __global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __rest
 
 // ---- bin reduction: W = sum_t (t+1) S_t and T = sum_t S_t over a bin's 256 bucket sums ----
 // Lane-parallel (every lane adds its own points; quad-cooperative arithmetic would spend a whole
-// wave-instruction on 16 additions instead of 64): RED_LANES lanes per bin, RED_CHUNK = 256 /
-// RED_LANES consecutive buckets per lane, 64 / RED_LANES bins per wave. Lane j runs the chunk's
-// running sums from the top bucket down (s_j = sum_i B_i, r_j = sum_i (i+1) B_i), then the lanes
-// of a bin combine through shuffles: sum_t (t+1) B_t = sum_j r_j + RED_CHUNK * sum_{j>=1} Suf_j with
-// Suf_j = sum_{k>=j} s_k (a suffix scan), and T = Suf_0.
-#ifndef EDC_RED_LANES
-#define EDC_RED_LANES 32
-#endif
-constexpr int RED_LANES = EDC_RED_LANES;
-constexpr int RED_CHUNK = NSLICE / RED_LANES;
-constexpr int RED_BINS_PER_WG = 256 / RED_LANES;
-
+// wave-instruction on 16 additions instead of 64): L lanes per bin, 256 / L consecutive buckets
+// per lane, 64 / L bins per wave. Lane j runs the chunk's running sums from the top bucket down
+// (s_j = sum_i B_i, r_j = sum_i (i+1) B_i), then the lanes of a bin combine through shuffles:
+// sum_t (t+1) B_t = sum_j r_j + (256 / L) * sum_{j>=1} Suf_j with Suf_j = sum_{k>=j} s_k (a suffix
+// scan), and T = Suf_0. L = 32 for large batches (least work: 1-2 workgroups per CU anyway);
+// L = 64 when there are few bins and the serial depth (2 * 256 / L + 2 log2 L + log2(256 / L)
+// additions) is the latency of the whole pass.
+template <int L>
 __device__ __forceinline__ fe shfl_down_fe(const fe& a, int d) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)__shfl_down((int)a.v[i], d, RED_LANES);
+  for (int i = 0; i < 9; ++i) r.v[i] = (uint32_t)__shfl_down((int)a.v[i], d, L);
   return r;
 }
+template <int L>
 __device__ __forceinline__ ge_p3 shfl_down_pt(const ge_p3& P, int d) {
-  return ge_p3{shfl_down_fe(P.X, d), shfl_down_fe(P.Y, d), shfl_down_fe(P.Z, d), shfl_down_fe(P.T, d)};
+  return ge_p3{shfl_down_fe<L>(P.X, d), shfl_down_fe<L>(P.Y, d), shfl_down_fe<L>(P.Z, d), shfl_down_fe<L>(P.T, d)};
 }
 
+template <int L>
 __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ buckets,
                                                     uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
-  const uint32_t bin = blockIdx.x * RED_BINS_PER_WG + threadIdx.x / RED_LANES;
-  const int j = (int)(threadIdx.x % RED_LANES);
+  constexpr int CHUNK = NSLICE / L;
+  const uint32_t bin = blockIdx.x * (256 / L) + threadIdx.x / L;
+  const int j = (int)(threadIdx.x % L);
   const bool live = bin < nbin && counts[bin] != 0;     // empty bins: the accumulation wrote W = T = 0
   ge_p3 run = ge_identity(), acc = ge_identity();
   if (live) {
-    const uint32_t* base = buckets + ((size_t)bin * NSLICE + (size_t)j * RED_CHUNK) * EXT_WORDS;
-    ge_p3 nxt = ld_ext(base + (RED_CHUNK - 1) * EXT_WORDS);
+    const uint32_t* base = buckets + ((size_t)bin * NSLICE + (size_t)j * CHUNK) * EXT_WORDS;
+    ge_p3 nxt = ld_ext(base + (CHUNK - 1) * EXT_WORDS);
     run = nxt;
     acc = nxt;
-    for (int i = RED_CHUNK - 2; i >= 0; --i) {
+    for (int i = CHUNK - 2; i >= 0; --i) {
       const ge_p3 cur = ld_ext(base + i * EXT_WORDS);
       run = ge_add(run, cur);
       acc = ge_add(acc, run);
@@ -483,19 +482,19 @@ __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_
   }
   // suffix scan of s_j = run over the bin's lanes (all lanes of a wave take part in the shuffles)
   ge_p3 suf = run;
-  for (int d = 1; d < RED_LANES; d <<= 1) {
-    const ge_p3 o = shfl_down_pt(suf, d);
-    if (j + d < RED_LANES) suf = ge_add(suf, o);
+  for (int d = 1; d < L; d <<= 1) {
+    const ge_p3 o = shfl_down_pt<L>(suf, d);
+    if (j + d < L) suf = ge_add(suf, o);
   }
-  // x_j = r_j + RED_CHUNK * Suf_j (j >= 1), x_0 = r_0; then the sum over the bin's lanes
+  // x_j = r_j + CHUNK * Suf_j (j >= 1), x_0 = r_0; then the sum over the bin's lanes
   ge_p3 x = acc;
   if (j >= 1) {
     ge_p3 y = suf;
-    for (int k = 1; k < RED_CHUNK; k <<= 1) y = ge_dbl(y);
+    for (int k = 1; k < CHUNK; k <<= 1) y = ge_dbl(y);
     x = ge_add(x, y);
   }
-  for (int d = RED_LANES / 2; d >= 1; d >>= 1) {
-    const ge_p3 o = shfl_down_pt(x, d);
+  for (int d = L / 2; d >= 1; d >>= 1) {
+    const ge_p3 o = shfl_down_pt<L>(x, d);
     if (j < d) x = ge_add(x, o);
   }
   if (live && j == 0) {
@@ -679,8 +678,12 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
                      buckets);
   hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
                      buckets, heads, slice_W, slice_T);
-  hipLaunchKernelGGL(k_msm_reduce, dim3(cdiv(P.nbin(), RED_BINS_PER_WG)), dim3(256), 0, st, P.nbin(), counts, buckets,
-                     slice_W, slice_T);
+  if (P.nbin() < 512)
+    hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
+                       slice_T);
+  else
+    hipLaunchKernelGGL(k_msm_reduce<32>, dim3(cdiv(P.nbin(), 8)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
+                       slice_T);
 }
 
 #ifdef EDC_STAMPS
