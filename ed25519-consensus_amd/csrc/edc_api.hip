@@ -539,17 +539,13 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   auto mark = [&](int ph) {
     if (s.timed) (void)hipEventRecord(s.ev[ph], st);
   };
-  CK(hipMemsetAsync(s.flags, 0, FLAG_COUNT * sizeof(int), st));
-  CK(hipMemsetAsync(s.u_acc, 0, KEY_ACC_LIMBS * sizeof(unsigned long long), st));
-  CK(hipMemsetAsync(s.d_out, 0, 256, st));
   const bool per_sig = force_per_sig || choose_per_sig(ctx, n);
   s.per_sig = per_sig;
   s.n_batch = N;
   mark(PH_KEYS);
-  if (per_sig) {
-    launch_keys_per_sig(st, N, s.flags);
-  } else {
-    CK(hipMemsetAsync(s.table, 0xFF, (size_t)T * sizeof(uint32_t), st));
+  launch_init_batch(st, s.flags, per_sig ? (int)N : -1, s.u_acc, s.d_out, per_sig ? nullptr : s.table, per_sig ? 0u : T,
+                    with_bin ? s.counts : nullptr, with_bin ? P->nbin() : 0u);
+  if (!per_sig) {
     const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
     const uint32_t salt[2] = {(uint32_t)h, (uint32_t)(h >> 32)};
     launch_keys(st, N, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
@@ -562,7 +558,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
               per_sig, s.coef_part);
   mark(PH_MSM_BIN);
   if (with_bin) launch_msm_bin(st, *P, batch_terms(*P, s, N), 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries,
-                              s.flags);
+                              s.flags, true);
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);

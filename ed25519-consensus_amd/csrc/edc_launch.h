@@ -16,7 +16,6 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
                  uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags);
 // per-signature key terms (no grouping): m = n, key j is signature j's own key (key_rep = null)
-void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags);
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
@@ -36,9 +35,13 @@ void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const 
 // vk_out[i] = keys[reg[key_idx[i]]] (32 bytes each; key-indexed host submissions)
 void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, const uint32_t* reg,
                         const uint32_t* keys, uint8_t* vk_out);
-// edc_msm.hip
+// per-batch resets in one launch: flags (FLAG_NKEYS = nkeys if >= 0), u_acc, the 256-byte result
+// block, table[0..T) = 0xFFFFFFFF, counts[0..nbin) = 0 (T / nbin may be 0)
+void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long* u_acc, uint8_t* d_out, uint32_t* table,
+                       uint32_t T, uint32_t* counts, uint32_t nbin);
+// edc_msm.hip (counts_zeroed: the caller already cleared counts, e.g. launch_init_batch)
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
-                    uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags);
+                    uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed = false);
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T);

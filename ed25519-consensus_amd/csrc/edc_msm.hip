@@ -654,9 +654,9 @@ __global__ void k_combine(uint32_t g, const uint8_t* __restrict__ partials, int 
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
-                    uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags) {
+                    uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed) {
   const uint32_t nbin = P.nbin();
-  (void)hipMemsetAsync(counts, 0, nbin * sizeof(uint32_t), st);
+  if (!counts_zeroed) (void)hipMemsetAsync(counts, 0, nbin * sizeof(uint32_t), st);
   // terms per workgroup: up to 4096 (long runs of entries per bin for the scatter's writes), but
   // at least ~256 workgroups so small batches still fill the GPU
   uint32_t per = max_terms / 256;

@@ -544,9 +544,29 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index, flags);
 }
-void launch_keys_per_sig(hipStream_t st, uint32_t n, int* flags) {
-  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags + FLAG_NKEYS), (int)n, 1, st);
+// One launch for the per-batch resets (flags, global coefficient sums, result block, key table,
+// MSM bin counts) instead of five runtime fills: each fill is a launch of its own, ~8 us apiece in
+// the latency of a small batch.
+__global__ void __launch_bounds__(256) k_init_batch(int* __restrict__ flags, int nkeys, unsigned long long* __restrict__ u_acc,
+                                                    uint32_t* __restrict__ d_out, uint32_t* __restrict__ table, uint32_t T,
+                                                    uint32_t* __restrict__ counts, uint32_t nbin) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  if (i < FLAG_COUNT) flags[i] = (i == FLAG_NKEYS && nkeys >= 0) ? nkeys : 0;
+  if (i < KEY_ACC_LIMBS) u_acc[i] = 0;
+  if (i < 64) d_out[i] = 0;
+  for (uint32_t j = i; j < T; j += stride) table[j] = 0xFFFFFFFFu;
+  for (uint32_t j = i; j < nbin; j += stride) counts[j] = 0;
 }
+
+void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long* u_acc, uint8_t* d_out, uint32_t* table,
+                       uint32_t T, uint32_t* counts, uint32_t nbin) {
+  const uint32_t work = T > nbin ? T : nbin;
+  uint32_t grid = cdiv(work > 256 ? work : 256, 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(k_init_batch, dim3(grid), dim3(256), 0, st, flags, nkeys, u_acc, reinterpret_cast<uint32_t*>(d_out),
+                     table, T, counts, nbin);
+}
+
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
