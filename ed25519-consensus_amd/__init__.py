@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_set_key_grouping", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
+    "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
 ]
@@ -151,6 +151,7 @@ def load_library(path=None):
         lib.edc_keycache_size.restype = c_sz
         lib.edc_keycache_size.argtypes = [c_vp]
         lib.edc_set_key_grouping.argtypes = [c_vp, ctypes.c_int]
+        lib.edc_set_key_split.argtypes = [c_vp, ctypes.c_int]
         if path is None:
             _lib = lib
         return lib
@@ -320,6 +321,11 @@ class Engine:
         """0 auto (default), 1 always group keys, 2 never (one A term per signature), 3 test mode:
         grouping abandoned on the device (the adversarial-key overflow path)."""
         self._check(self.lib.edc_set_key_grouping(self.ctx, int(mode)))
+
+    def set_key_split(self, mode):
+        """0 auto (default): split B / key coefficients at bit 128 onto the key cache's [2^128]A
+        while the cache covers the batches' keys; 1 never."""
+        self._check(self.lib.edc_set_key_split(self.ctx, int(mode)))
 
     def set_msm_shape(self, bits=0, parts=0):
         """Pippenger window width (8..16) and parts (1..64); 0 = chosen from the batch size."""

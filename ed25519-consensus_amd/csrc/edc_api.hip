@@ -115,10 +115,14 @@ struct edc_ctx {
   uint32_t kc_m = 0, kc_tmask = 0;
   uint32_t* kc_reg = nullptr;   // registered position -> cache index (edc_batch_submit_indexed)
   uint32_t kc_reg_m = 0;
+  // split coefficients (edc_common.h) while the key cache covers the batches' keys:
+  // key_split 0 = auto, 1 = never; last_uncached = keys the last batch did not find in the cache
+  int key_split = 0;
+  uint32_t last_uncached = 0;
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
-    if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0};
-    return KeyCacheView{kc_table, kc_keys, kc_ok, kc_comb, kc_tmask, kc_m};
+    if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr};
+    return KeyCacheView{kc_table, kc_keys, kc_ok, kc_comb, kc_tmask, kc_m, bcomb};
   }
 };
 
@@ -202,8 +206,9 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.key_rep, cap));
   CK(dalloc(&s.table, T));
   CK(dalloc(&s.slot_key, T));
-  CK(dalloc(&s.pts, (2 + 2 * cap) * NIELS_WORDS));   // >= msm_num_points(n, m) for any m <= n
-  CK(dalloc(&s.scal, (2 + 2 * cap) * 8));
+  // >= msm_num_points_split(n, m) for any m <= n (split coefficients add m + 1 points)
+  CK(dalloc(&s.pts, (3 + 3 * cap) * NIELS_WORDS));
+  CK(dalloc(&s.scal, (3 + 3 * cap) * 8));
   CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
   CK(dalloc(&s.u_acc, (cap / COEF_CHUNK + 2) * KEY_ACC_LIMBS));   // one sum per fallback range
   CK(dalloc(&s.coef_part, coef_part_words(cap)));
@@ -285,7 +290,7 @@ static void plan_layout(MsmPlan& P) {
   P.bins_per_range = bin;
 }
 
-static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
+static MsmPlan make_plan(int c, int hi, uint32_t nranges, bool hi_windows = true) {
   MsmPlan P{};
   uint32_t w = 0, off = 0;
   auto add = [&](uint32_t bits, uint32_t buckets) {
@@ -302,7 +307,7 @@ static MsmPlan make_plan(int c, int hi, uint32_t nranges) {
     add(bits, i + 1 == ws ? (1u << bits) : (1u << (bits - 1)));
   }
   P.nwin_short = ws;
-  const uint32_t wh = (125 + hi - 1) / hi;
+  const uint32_t wh = hi_windows ? (125 + hi - 1) / hi : 0;
   for (uint32_t i = 0; i < wh; ++i) {
     const uint32_t bits = 125 / wh + (i < 125 % wh ? 1 : 0);
     add(bits, i + 1 == wh ? (1u << bits) : (1u << (bits - 1)));
@@ -326,10 +331,10 @@ static uint32_t floor_pow2(double x) {
 // index, summed per slice by k_msm_window) so that every bin holds about the same number of
 // entries and ~1-2k workgroups accumulate. edc_set_msm_shape's parts instead split the whole batch.
 // Any plan is an exact MSM: the hint and the split only affect speed.
-static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
+static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig, bool split = false) {
   const int c = ctx->win_bits ? ctx->win_bits : auto_window_bits(n);
   const bool few = !per_sig && ctx->have_key_ratio && ctx->last_key_ratio * 16.0 <= 1.0 && n >= 4096;
-  MsmPlan P = make_plan(c, few ? 8 : c, 1);
+  MsmPlan P = make_plan(c, few ? 8 : c, 1, !split);
   if (ctx->msm_parts) {
     uint32_t parts = ctx->msm_parts;
     while (parts > 1 && P.bins_per_range * parts > MSM_MAX_BINS) parts /= 2;
@@ -347,11 +352,12 @@ static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
   double dens[MSM_MAX_WIN], total = 0;
   for (uint32_t w = 0; w < P.nwin; ++w) {
     const double sl = P.nslice[w], half = sl > 1 ? sl / 2 : 1;
-    if (w + 1 < P.nwin_short) dens[w] = (ns + nf) / sl;
+    if (split) dens[w] = (ns + 2 * nf) / sl;      // every term short, top windows unsigned
+    else if (w + 1 < P.nwin_short) dens[w] = (ns + nf) / sl;
     else if (w + 1 == P.nwin_short) dens[w] = ns / sl + nf / half;
     else if (w + 1 < P.nwin) dens[w] = nf / sl;
     else dens[w] = nf / half;
-    total += (w < P.nwin_short ? ns + nf : nf);
+    total += split ? ns + 2 * nf : (w < P.nwin_short ? ns + nf : nf);
   }
   double target = ctx->bin_entries ? (double)ctx->bin_entries : (total / 1024.0 > 4096.0 ? total / 1024.0 : 4096.0);
   for (;;) {
@@ -363,8 +369,16 @@ static MsmPlan batch_plan(const edc_ctx* ctx, size_t n, bool per_sig) {
   return P;
 }
 
-static MsmTerms batch_terms(const MsmPlan& P, const Slot& s, uint32_t n) {
-  return MsmTerms{n, 0, 0, 0, P.sum_ranges ? P.nranges : 1u, s.scal, nullptr, nullptr, nullptr};
+static MsmTerms batch_terms(const MsmPlan& P, const Slot& s, uint32_t n, bool split) {
+  return MsmTerms{n, 0, 0, 0, P.sum_ranges ? P.nranges : 1u, s.scal, nullptr, nullptr, nullptr, split ? 1u : 0u};
+}
+
+// Split coefficients need [2^128]A of every key of the batch; the cache holds it for registered
+// keys. They are planned while the previous batch found all its keys in the cache (a key missing
+// from it still verifies exactly: k_decompress doubles it 128 times, and the next batches go back
+// to the wide-coefficient plan until a batch finds every key again).
+static bool choose_split(const edc_ctx* ctx) {
+  return ctx->kc_m && ctx->bcomb && ctx->key_split == 0 && ctx->last_uncached == 0;
 }
 
 // host-staging buffers (inputs of the host-pointer entry points, per-item outputs)
@@ -525,7 +539,8 @@ static bool choose_per_sig(const edc_ctx* ctx, size_t n) {
 // z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization.
 static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
-                          const uint8_t* d_z, bool with_bin, const MsmPlan* P, bool force_per_sig = false) {
+                          const uint8_t* d_z, bool with_bin, const MsmPlan* P, bool force_per_sig = false,
+                          bool split = false) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
@@ -555,14 +570,15 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
   launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
-              per_sig, s.coef_part);
+              per_sig, s.coef_part, split);
   mark(PH_MSM_BIN);
-  if (with_bin) launch_msm_bin(st, *P, batch_terms(*P, s, N), 1 + 2 * N, s.counts, s.offsets, s.cursor, s.entries,
-                              s.flags, true);
+  if (with_bin)
+    launch_msm_bin(st, *P, batch_terms(*P, s, N, split), split ? 2 + 3 * N : 1 + 2 * N, s.counts, s.offsets, s.cursor,
+                   s.entries, s.flags, true);
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
-  launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc());
+  launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc(), split);
   CK(hipGetLastError());
   return 0;
 }
@@ -574,10 +590,11 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
-  const MsmPlan P = batch_plan(ctx, n, choose_per_sig(ctx, n));
-  rc = ensure_msm(ctx, s, P, msm_entry_capacity(P, n, n + 1));
+  const bool per_sig = choose_per_sig(ctx, n), split = choose_split(ctx);
+  const MsmPlan P = batch_plan(ctx, n, per_sig, split);
+  rc = ensure_msm(ctx, s, P, split ? msm_entry_capacity(P, 2 + 3 * n, 0) : msm_entry_capacity(P, n, n + 1));
   if (rc) return rc;
-  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P);
+  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P, per_sig, split);
   if (rc) return rc;
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
@@ -611,6 +628,7 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
       ctx->have_key_ratio = true;
       ctx->last_key_ratio = (double)reinterpret_cast<int*>(s.h_out)[2] / (double)s.n_batch;
     }
+    if (ctx->kc_m) ctx->last_uncached = (uint32_t)reinterpret_cast<int*>(s.h_out)[44];
   }
   if (check8) {
     if (bad) memset(check8, 0, 32);
@@ -1175,6 +1193,7 @@ int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok
   CK(hipStreamSynchronize(st));
   (void)hipFree(ext);
   ctx->kc_m = u;
+  ctx->last_uncached = 0;                    // try split coefficients with the new key set
   ctx->kc_tmask = T - 1;
   ctx->kc_reg_m = (uint32_t)m;
   if (ok)
@@ -1244,6 +1263,12 @@ int edc_set_key_grouping(edc_ctx* ctx, int mode) {
   return 0;
 }
 
+int edc_set_key_split(edc_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 1) return EDC_ERR_ARG;
+  ctx->key_split = mode;
+  return 0;
+}
+
 int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits) {
   if (!ctx || ranges < 1 || ranges > 1024 || bits < 8 || bits > 13) return EDC_ERR_ARG;
   ctx->fb_ranges = (uint32_t)ranges;
@@ -1272,7 +1297,10 @@ int edc_reserve(edc_ctx* ctx, size_t n) {
   dense.nranges = few.nranges = MSM_MAX_BINS / (dense.bins_per_range > few.bins_per_range ? dense.bins_per_range
                                                                                           : few.bins_per_range);
   if (dense.nranges > 16) dense.nranges = few.nranges = 16;
-  const size_t e1 = msm_entry_capacity(dense, n, n + 1), e2 = msm_entry_capacity(few, n, n + 1);
+  const MsmPlan splitp = make_plan(c, c, 1, false);
+  size_t e1 = msm_entry_capacity(dense, n, n + 1), e2 = msm_entry_capacity(few, n, n + 1);
+  const size_t e3 = msm_entry_capacity(splitp, 2 + 3 * n, 0);   // split coefficients (key cache)
+  if (e3 > e1) e1 = e3;
   for (Slot& s : ctx->slot) {
     if (s.pending) { ctx->err = "reserve with a batch in flight"; return EDC_ERR_ARG; }
     int rc = ensure_slot(ctx, s, n);

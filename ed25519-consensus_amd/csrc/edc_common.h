@@ -108,6 +108,7 @@ struct MsmTerms {
   const uint32_t* xpt;
   const uint32_t* xrg;
   const uint32_t* xscal;
+  uint32_t split;                 // batch with split coefficients (msm_num_points_split): all terms short
 };
 
 // signed digit of window w (bits <= 16) with carry in/out; top_unsigned keeps the raw value
@@ -127,11 +128,22 @@ constexpr int KEY_ACC_LIMBS = 12;
 
 // flags slot indices. FLAG_OVF: key grouping gave up (probe limit, section "Key grouping" of
 // DESIGN.md): the batch continues with one key term per signature, which is the same group element.
-enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_COUNT = 8 };
+// FLAG_UNCACHED: keys of the batch not found in the context's key cache (reported to the host,
+// which only plans split coefficients while the previous batch had none).
+enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_UNCACHED = 4, FLAG_COUNT = 8 };
 
 // Points of a batch MSM: 0 = B, 1..n = R_i, n+1..n+m = the distinct keys (grouped) or each
 // signature's own key (m = n, one key term per signature).
 __host__ __device__ __forceinline__ uint32_t msm_num_points(uint32_t n, uint32_t m) { return 1 + n + m; }
+
+// Split coefficients (a batch whose keys are all in the context's key cache): every 253-bit
+// coefficient c of B and of the keys is written c = lo + 2^128 hi, lo on the point itself and hi on
+// its [2^128] multiple, which the cache holds (comb[32][0] = [16^32]A). Every term is then at most
+// 128 bits, the plan has no windows above bit 128 and the Horner chain is ~128 doublings instead of
+// ~250. Points: 0 = B, 1..n = R_i, 1+n..n+m = A_j, 1+n+m = [2^128]B, 2+n+m+j = [2^128]A_j.
+__host__ __device__ __forceinline__ uint32_t msm_num_points_split(uint32_t n, uint32_t m) { return 2 + n + 2 * m; }
+__host__ __device__ __forceinline__ uint32_t split_hi_point(uint32_t n, uint32_t m, uint32_t j) { return 2 + n + m + j; }
+__host__ __device__ __forceinline__ uint32_t split_b_hi_point(uint32_t n, uint32_t m) { return 1 + n + m; }
 
 constexpr int BTAB_ENTRIES = 8;
 constexpr uint32_t COEF_CHUNK = 2048;   // signatures per k_coef workgroup (range sizes are multiples)   // context table [1..8]B (per-item fallback, signer)

@@ -11,7 +11,7 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
-                       const KeyCacheView& kc);
+                       const KeyCacheView& kc, bool split = false);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
                  uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags);
@@ -19,7 +19,7 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig, uint32_t* coef_part);
+                 bool per_sig, uint32_t* coef_part, bool split = false);
 // words of k_coef's per-workgroup key-slot dump for batches of up to cap_n signatures
 size_t coef_part_words(size_t cap_n);
 // grouped fallback: per-(range, key) / per-range coefficients as listed MSM terms

@@ -20,7 +20,9 @@ namespace edc {
 
 
 __device__ __forceinline__ uint32_t terms_count(const MsmTerms& T, const int* flags) {
-  return T.rsize ? T.npoint + T.nx : msm_num_points(T.n, (uint32_t)flags[FLAG_NKEYS]);
+  if (T.rsize) return T.npoint + T.nx;
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  return T.split ? msm_num_points_split(T.n, m) : msm_num_points(T.n, m);
 }
 
 // term t -> point index, range, short scalar?, scalar words
@@ -30,7 +32,7 @@ __device__ __forceinline__ void term_get(const MsmTerms& T, uint32_t t, uint32_t
   if (!T.rsize) {
     pt = t;
     rg = T.nparts > 1 ? t % T.nparts : 0;   // interleaved: every part gets its share of R, keys and B
-    shrt = t >= 1 && t <= T.n;
+    shrt = T.split || (t >= 1 && t <= T.n);
     src = T.scal + (size_t)t * 8;
   } else if (t < T.npoint) {       // R_i (t < n), then one key term per signature
     pt = 1 + t;
@@ -621,6 +623,7 @@ __global__ void k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W, con
   reinterpret_cast<int*>(out)[1] = bad;
   reinterpret_cast<int*>(out)[2] = flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
   reinterpret_cast<int*>(out)[3] = flags[FLAG_OVF];
+  reinterpret_cast<int*>(out)[44] = flags[FLAG_UNCACHED];   // byte 176, after the partial point
   if (want_compress) {
     uint32_t w8[8];
     ge_compress(c8, w8);

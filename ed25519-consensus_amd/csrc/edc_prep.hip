@@ -69,12 +69,25 @@ __device__ __forceinline__ void copy_record(uint32_t* __restrict__ pts, uint32_t
   for (int i = 0; i < NIELS_WORDS / 4; ++i) d[i] = q[i];
 }
 
+// [2^128]P as affine Niels (split coefficients, a key missing from the cache: the slow path; the
+// host stops planning split coefficients after such a batch)
+__device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
+  for (int k = 0; k < 128; ++k) P = ge_dbl(P, k == 127);
+  const fe zi = fe_invert(P.Z);
+  ge_p3 A;
+  A.X = fe_mul(P.X, zi);
+  A.Y = fe_mul(P.Y, zi);
+  A.Z = fe_one();
+  A.T = fe_mul(A.X, A.Y);
+  return ge_to_niels_affine(A);
+}
+
 __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep, int per_sig_host,
                                                        uint32_t* __restrict__ pts, uint8_t* __restrict__ itembad,
                                                        uint8_t* __restrict__ keybad, int* __restrict__ flags,
-                                                       KeyCacheView kcache) {
+                                                       KeyCacheView kcache, int split) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t w[8];
   if (i < n) {
@@ -89,19 +102,25 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t
     return;
   }
   const uint32_t j = i - n;
-  if (j >= (uint32_t)flags[FLAG_NKEYS]) return;
+  const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
+  if (j >= m) return;
   const bool per_sig = per_sig_host || flags[FLAG_OVF];
   ld_words8(vk + (size_t)(per_sig ? j : key_rep[j]) * 32, w);
   const int ci = kc_lookup(kcache, w);
   bool ok;
   if (ci >= 0) {                    // registered key: A = comb[0][0], decoded once per context
-    copy_record(pts, 1 + n + j, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS);
+    const uint32_t* comb = kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS;
+    copy_record(pts, 1 + n + j, comb);
+    if (split) copy_record(pts, split_hi_point(n, m, j), comb + (size_t)COMB_SHIFT128 * NIELS_WORDS);
     ok = kcache.ok[ci] != 0;
   } else {
     ge_p3 P;
     ok = ge_decompress(w, P);
     st_niels(pts, 1 + n + j, ge_to_niels_affine(P));
+    if (kcache.table) atomicAdd(&flags[FLAG_UNCACHED], 1);
+    if (split) st_niels(pts, split_hi_point(n, m, j), shift128_niels(P));
   }
+  if (split && j == 0) copy_record(pts, split_b_hi_point(n, m), kcache.bcomb + (size_t)COMB_SHIFT128 * NIELS_WORDS);
   keybad[j] = ok ? 0 : 1;
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
 }
@@ -272,7 +291,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               unsigned long long* __restrict__ u_acc,
                                               uint8_t* __restrict__ itembad,
                                               int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m,
-                                              uint32_t* __restrict__ coef_part) {
+                                              uint32_t* __restrict__ coef_part, int split) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
@@ -336,7 +355,14 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
         const sc a = sc_reduce_wide(x);
         uint4* ap = reinterpret_cast<uint4*>(scal + (size_t)(1 + n + i) * 8);
         ap[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-        ap[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+        if (split) {                 // lo on A_i, hi on [2^128]A_i (key layout m = n)
+          ap[1] = make_uint4(0, 0, 0, 0);
+          uint4* hp = reinterpret_cast<uint4*>(scal + (size_t)split_hi_point(n, n, i) * 8);
+          hp[0] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+          hp[1] = make_uint4(0, 0, 0, 0);
+        } else {
+          ap[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+        }
         continue;
       }
       const uint32_t key = pair0 + key_index[i];
@@ -463,16 +489,36 @@ __device__ __forceinline__ void store_scalar(uint32_t* scal, size_t idx, const s
   d[1] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
 }
 
-// Batch: A_coeff of key j = sum z k mod l -> scalar of point n+1+j; B_coeff = -sum z s -> point 0.
+// c = lo + 2^128 hi: lo -> scalar lo_idx, hi -> scalar hi_idx (split coefficients, edc_common.h)
+__device__ __forceinline__ void store_split(uint32_t* scal, size_t lo_idx, size_t hi_idx, const sc& c) {
+  uint4* l = reinterpret_cast<uint4*>(scal + lo_idx * 8);
+  uint4* h = reinterpret_cast<uint4*>(scal + hi_idx * 8);
+  l[0] = make_uint4(c.v[0], c.v[1], c.v[2], c.v[3]);
+  l[1] = make_uint4(0, 0, 0, 0);
+  h[0] = make_uint4(c.v[4], c.v[5], c.v[6], c.v[7]);
+  h[1] = make_uint4(0, 0, 0, 0);
+}
+
+// Batch: A_coeff of key j = sum z k mod l -> scalar of point n+1+j; B_coeff = -sum z s -> point 0
+// (split: the high halves go to the [2^128] points).
 __global__ void __launch_bounds__(256) k_key_final(uint32_t n, const unsigned long long* __restrict__ key_acc,
                                                    const unsigned long long* __restrict__ u_acc,
                                                    uint32_t* __restrict__ scal,
-                                                   const int* __restrict__ flags, int per_sig_host) {
+                                                   const int* __restrict__ flags, int per_sig_host, int split) {
   const uint32_t j0 = blockIdx.x * blockDim.x + threadIdx.x;
   const bool per_sig = per_sig_host || flags[FLAG_OVF];
-  const uint32_t m = per_sig ? 0u : (uint32_t)flags[FLAG_NKEYS];
-  for (uint32_t j = j0; j < m; j += gridDim.x * blockDim.x) store_scalar(scal, 1 + n + j, reduce_limb_sums(key_acc + (size_t)j * PL));
-  if (j0 == 0) store_scalar(scal, 0, sc_sub(sc_zero(), reduce_limb_sums(u_acc)));
+  const uint32_t mk = (uint32_t)flags[FLAG_NKEYS];          // key points of the layout
+  const uint32_t m = per_sig ? 0u : mk;                     // keys whose sums are reduced here
+  for (uint32_t j = j0; j < m; j += gridDim.x * blockDim.x) {
+    const sc c = reduce_limb_sums(key_acc + (size_t)j * PL);
+    if (split) store_split(scal, 1 + n + j, split_hi_point(n, mk, j), c);
+    else store_scalar(scal, 1 + n + j, c);
+  }
+  if (j0 == 0) {
+    const sc b = sc_sub(sc_zero(), reduce_limb_sums(u_acc));
+    if (split) store_split(scal, 0, split_b_hi_point(n, mk), b);
+    else store_scalar(scal, 0, b);
+  }
 }
 
 // Range mode (grouped fallback): listed MSM terms (point, range, scalar). Pairs q = g m + j
@@ -524,11 +570,11 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
 }
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
-                       const KeyCacheView& kc) {
+                       const KeyCacheView& kc, bool split) {
   // lanes [0, n) decode R_i, lanes [n, 2n) cover the largest possible key count (m <= n)
   if (n)
     hipLaunchKernelGGL(k_decompress, dim3(cdiv(2ull * n, 256)), dim3(256), 0, st, n, sig, vk, key_rep,
-                       per_sig ? 1 : 0, pts, itembad, keybad, flags, kc);
+                       per_sig ? 1 : 0, pts, itembad, keybad, flags, kc, split ? 1 : 0);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
@@ -570,18 +616,18 @@ void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig, uint32_t* coef_part) {
+                 bool per_sig, uint32_t* coef_part, bool split) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
   if (n) {
     const uint32_t nwg = cdiv(n, COEF_CHUNK);
     uint32_t* part = per_sig ? nullptr : coef_part;
     hipLaunchKernelGGL(k_coef, dim3(nwg), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index, scal, key_acc,
-                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part);
+                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part, split ? 1 : 0);
     if (part) hipLaunchKernelGGL(k_coef_merge, dim3(COEF_SLOTS), dim3(256), 0, st, nwg, part, key_acc);
   }
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
-                     u_acc, scal, flags, per_sig ? 1 : 0);
+                     u_acc, scal, flags, per_sig ? 1 : 0, split ? 1 : 0);
 }
 size_t coef_part_words(size_t cap_n) {
   const size_t nwg = (cap_n + COEF_CHUNK - 1) / COEF_CHUNK;
@@ -600,7 +646,7 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
                        key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm,
-                       (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, 0);
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }

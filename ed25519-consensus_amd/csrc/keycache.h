@@ -7,8 +7,8 @@
 // key, a fixed-base comb table
 //     comb[j][d-1] = [d * 16^j] A    (j = 0..63, d = 1..8), affine Niels, 512 records = 64 KB
 // so that
-//   - a batch takes A (= comb[0][0]) and, in few-key mode, [2^128]A (= comb[32][0]) from the
-//     cache instead of decoding / doubling them;
+//   - a batch takes A (= comb[0][0]) and, with split coefficients (edc_common.h), [2^128]A
+//     (= comb[32][0]) from the cache instead of decoding / doubling them;
 //   - the per-item fallback computes [s]B - [k]A as 128 mixed additions and NO doublings
 //     (signed radix-16 digits, one comb record each for k and s), against 252 doublings + 128
 //     additions + one A decode + 7 table additions per item without the cache.
@@ -34,6 +34,7 @@ struct KeyCacheView {
   const uint32_t* comb;    // m x COMB_ENTRIES affine Niels records
   uint32_t tmask;
   uint32_t m;
+  const uint32_t* bcomb;   // COMB_ENTRIES records of B (built with the first cache)
 };
 
 __host__ __device__ inline uint32_t kc_hash(const uint32_t w[8]) {

@@ -80,7 +80,7 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
 /*
  * Asynchronous form of edc_batch_verify_device for streams of batches (a consensus node
  * verifying block after block): edc_batch_submit_device enqueues the whole pipeline on one of the
- * context's in-flight slots (4) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
+ * context's in-flight slots (8) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
  * ticket and returns its verdict (EDC_OK / EDC_INVALID_SIGNATURE, <0 on runtime failure), with
  * optional check8 (needs want_check8), partial point and bad flag. Tickets must be waited in
  * submission order before their slot is reused; inputs must stay valid until the wait.
@@ -248,6 +248,18 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
  * Every mode gives the same group element, hence identical verdicts and [8]*check.
  */
 int edc_set_key_grouping(edc_ctx* ctx, int mode);
+
+/*
+ * Split coefficients with the validator-key cache (edc_keycache_load). While the last batch found
+ * every key in the cache, mode 0 (default, auto) writes each 253-bit B / key coefficient as
+ * lo + 2^128 hi with hi on the cached [2^128]A (and [2^128]B), so every MSM term is 128 bits and
+ * the final Horner chain is ~128 doublings instead of ~250 (lower per-batch latency). A key
+ * missing from the cache still verifies exactly (it is doubled on the device) and turns the split
+ * off until a batch finds all its keys again. mode 1: never split. Same group element in every
+ * mode: identical verdicts and [8]*check. Replaces nothing in the reference (an MSM evaluation
+ * order, src/batch.rs:205-210).
+ */
+int edc_set_key_split(edc_ctx* ctx, int mode);
 
 /*
  * Pippenger shape for this context's batches (tuning / measurement): window width `bits` (8..16)

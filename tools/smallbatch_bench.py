@@ -29,6 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--sizes", default="8,16,24,32,40,48,56,64,150,1024")
+    ap.add_argument("--keycache", action="store_true",
+                    help="register the batch's keys in the context's key cache first (a node's validator set)")
     args = ap.parse_args()
     import torch
     import bench
@@ -58,6 +60,8 @@ def main():
             vks, sigs = eng.sign(distinct_seeds, msgs)
         else:
             vks, sigs = eng.sign([bytes([7]) * 32], msgs, seed_index=[0] * nmax)
+        if args.keycache:
+            eng.keycache_load(list(dict.fromkeys(vks)))
         for n in sizes:
             v, s, m = vks[:n], sigs[:n], msgs[:n]
             zs = bytes([0x33]) * 32
@@ -71,7 +75,8 @@ def main():
             t_dev = med_ms(lambda: eng._check(lib.edc_batch_verify_device(
                 eng.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(), d_off.data_ptr(), zs, 0, None,
                 None)))
-            row = {"n": n, "keys": kind, "gpu_batch_ms": round(t_batch, 4), "gpu_batch_dev_ms": round(t_dev, 4),
+            row = {"n": n, "keys": kind, "keycache": args.keycache, "gpu_batch_ms": round(t_batch, 4),
+                   "gpu_batch_dev_ms": round(t_dev, 4),
                    "gpu_batch_sigs_per_s": round(n / t_batch * 1e3, 1),
                    "cpu1_batch": oracle_c.bench_small(v, s, m, True)}
             if kind == "distinct":
