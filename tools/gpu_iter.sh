@@ -10,7 +10,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   rc=$?; echo "tests_rc=$rc"; tail -3 gpurun_out/gpu_tests.log
   [ $rc -eq 0 ] || exit $rc
 fi
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   AB_STEPS=${AB_STEPS:-40} bash tools/ab_variants.sh ${AB:-head base} || exit 1
 done
 if [ "${PMC:-0}" = 1 ]; then
