@@ -2,7 +2,7 @@
 // chains under several occupancy / ILP shapes and stamps the in-kernel clock
 // (s_memtime / s_memrealtime, MI355X_MICROARCH.md DVFS item 6), so the cost can be stated in
 // real shader cycles per wave-squaring per SIMD and compared with the instruction-issue sum.
-// Result (profiles/r01_sqr_probe.txt): ~380 cycles per wave-squaring at every occupancy (2-8
+// Result (profiles/r01_sqr_probe.txt, r02_sqr_probe_radix.txt, r02_sqr_probe_r25.txt): ~380 cycles per wave-squaring at every occupancy (2-8
 // waves/SIMD) and with two independent chains per lane, so the squaring is VALU-issue-bound;
 // 16 extra `s_nop 0` per squaring cost nothing (the hazard pads LLVM puts after inline asm are
 // free), and a hazard-aware hand schedule of every instruction (tried, not kept) ran the same.
@@ -196,6 +196,122 @@ __global__ void k_check_r32(uint32_t* bad, uint32_t s) {
   if (diff) atomicAdd(bad, 1u);
 }
 
+// ---- 5 x 51-bit limbs ("64-bit limbs" of the dalek u64 backend) on 32-bit multipliers: each
+// 51-bit limb is two 25.5-bit halves, i.e. ten limbs of 26 / 25 bits (weights 2^ceil(25.5 i)),
+// 2^255 == 19. A product f_i f_j lands in column i + j (mod 10) with factor 2 when i and j are
+// both odd and 19 when it wraps, so the squaring is 55 v_mad_u64_u32 over pre-doubled / x19 / x38
+// operands (all < 2^32), chained columns (carry of column k = addend of column k+1) and one
+// x19 fold of the top carry: 8 fewer products than radix 2^29 (63), two more column carries,
+// ~13 operand pre-multiplications.
+struct fe10 { uint32_t v[10]; };
+
+__device__ __forceinline__ uint32_t mul19(uint32_t x) { return (x << 4) + (x << 1) + x; }
+
+__device__ __forceinline__ fe10 sqr_r25(const fe10& a) {
+  const uint32_t* f = a.v;
+  const uint32_t f0_2 = f[0] << 1, f1_2 = f[1] << 1, f2_2 = f[2] << 1, f3_2 = f[3] << 1, f4_2 = f[4] << 1,
+                 f5_2 = f[5] << 1, f6_2 = f[6] << 1, f7_2 = f[7] << 1;
+  const uint32_t f6_19 = mul19(f[6]), f8_19 = mul19(f[8]);
+  const uint32_t f5_38 = mul19(f[5]) << 1, f7_38 = mul19(f[7]) << 1, f9_38 = mul19(f[9]) << 1;
+  fe10 r;
+  uint64_t acc;
+  acc = mad64(f[0], f[0], 0);
+  acc = mad64(f1_2, f9_38, acc); acc = mad64(f2_2, f8_19, acc); acc = mad64(f3_2, f7_38, acc);
+  acc = mad64(f4_2, f6_19, acc); acc = mad64(f[5], f5_38, acc);
+  r.v[0] = (uint32_t)acc & 0x3FFFFFFu; acc >>= 26;
+  acc = mad64(f0_2, f[1], acc); acc = mad64(f[2], f9_38, acc); acc = mad64(f3_2, f8_19, acc);
+  acc = mad64(f[4], f7_38, acc); acc = mad64(f5_2, f6_19, acc);
+  r.v[1] = (uint32_t)acc & 0x1FFFFFFu; acc >>= 25;
+  acc = mad64(f0_2, f[2], acc); acc = mad64(f1_2, f[1], acc); acc = mad64(f3_2, f9_38, acc);
+  acc = mad64(f4_2, f8_19, acc); acc = mad64(f5_2, f7_38, acc); acc = mad64(f[6], f6_19, acc);
+  r.v[2] = (uint32_t)acc & 0x3FFFFFFu; acc >>= 26;
+  acc = mad64(f0_2, f[3], acc); acc = mad64(f1_2, f[2], acc); acc = mad64(f[4], f9_38, acc);
+  acc = mad64(f5_2, f8_19, acc); acc = mad64(f[6], f7_38, acc);
+  r.v[3] = (uint32_t)acc & 0x1FFFFFFu; acc >>= 25;
+  acc = mad64(f0_2, f[4], acc); acc = mad64(f1_2, f3_2, acc); acc = mad64(f[2], f[2], acc);
+  acc = mad64(f5_2, f9_38, acc); acc = mad64(f6_2, f8_19, acc); acc = mad64(f[7], f7_38, acc);
+  r.v[4] = (uint32_t)acc & 0x3FFFFFFu; acc >>= 26;
+  acc = mad64(f0_2, f[5], acc); acc = mad64(f1_2, f[4], acc); acc = mad64(f2_2, f[3], acc);
+  acc = mad64(f[6], f9_38, acc); acc = mad64(f7_2, f8_19, acc);
+  r.v[5] = (uint32_t)acc & 0x1FFFFFFu; acc >>= 25;
+  acc = mad64(f0_2, f[6], acc); acc = mad64(f1_2, f5_2, acc); acc = mad64(f2_2, f[4], acc);
+  acc = mad64(f3_2, f[3], acc); acc = mad64(f7_2, f9_38, acc); acc = mad64(f[8], f8_19, acc);
+  r.v[6] = (uint32_t)acc & 0x3FFFFFFu; acc >>= 26;
+  acc = mad64(f0_2, f[7], acc); acc = mad64(f1_2, f[6], acc); acc = mad64(f2_2, f[5], acc);
+  acc = mad64(f3_2, f[4], acc); acc = mad64(f[8], f9_38, acc);
+  r.v[7] = (uint32_t)acc & 0x1FFFFFFu; acc >>= 25;
+  acc = mad64(f0_2, f[8], acc); acc = mad64(f1_2, f7_2, acc); acc = mad64(f2_2, f[6], acc);
+  acc = mad64(f3_2, f5_2, acc); acc = mad64(f[4], f[4], acc); acc = mad64(f[9], f9_38, acc);
+  r.v[8] = (uint32_t)acc & 0x3FFFFFFu; acc >>= 26;
+  acc = mad64(f0_2, f[9], acc); acc = mad64(f1_2, f[8], acc); acc = mad64(f2_2, f[7], acc);
+  acc = mad64(f3_2, f[6], acc); acc = mad64(f4_2, f[5], acc);
+  r.v[9] = (uint32_t)acc & 0x1FFFFFFu; acc >>= 25;
+  // top carry (weight 2^255 == 19) into limb 0, its overflow into limb 1
+  const uint64_t t = mad64((uint32_t)acc, 19u, (uint64_t)r.v[0]) + ((uint64_t)(uint32_t)(acc >> 32) * 19u << 32);
+  r.v[0] = (uint32_t)t & 0x3FFFFFFu;
+  r.v[1] += (uint32_t)(t >> 26);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t bits_at(const uint32_t w[8], int start, int len) {
+  const int k = start >> 5, sh = start & 31;
+  const uint64_t two = (uint64_t)w[k] | ((uint64_t)(k < 7 ? w[k + 1] : 0u) << 32);
+  return (uint32_t)(two >> sh) & ((1u << len) - 1u);
+}
+__device__ const int R25_OFF[11] = {0, 26, 51, 77, 102, 128, 153, 179, 204, 230, 255};
+
+__device__ fe10 fe10_from_words(const uint32_t w[8]) {
+  fe10 a;
+  for (int i = 0; i < 10; ++i) a.v[i] = bits_at(w, R25_OFF[i], R25_OFF[i + 1] - R25_OFF[i]);
+  return a;
+}
+// canonical 8 words of a lazy fe10 (serial carries, 2^255 == 19, then radix 2^29 canonicalisation)
+__device__ void fe10_to_words(fe10 a, uint32_t out[8]) {
+  for (int pass = 0; pass < 3; ++pass) {
+    uint32_t c = 0;
+    for (int i = 0; i < 10; ++i) {
+      const int len = R25_OFF[i + 1] - R25_OFF[i];
+      const uint64_t x = (uint64_t)a.v[i] + c;
+      a.v[i] = (uint32_t)x & ((1u << len) - 1u);
+      c = (uint32_t)(x >> len);
+    }
+    a.v[0] += 19u * c;
+  }
+  uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 10; ++i) {
+    const int st = R25_OFF[i], k = st >> 5, sh = st & 31;
+    w[k] |= a.v[i] << sh;
+    if (sh && k < 7) w[k + 1] |= (uint32_t)((uint64_t)a.v[i] >> (32 - sh));
+  }
+  fe z = fe_from_words(w);   // < 2^255
+  fe_to_words(z, out);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, W) k_sqr_r25(uint32_t* out, unsigned long long* clk, uint32_t s) {
+  uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  fe10 a;
+  for (int i = 0; i < 10; ++i) a.v[i] = ((s + blockIdx.x * 256 + threadIdx.x) * 2654435761u + i * 40503u) & 0x1FFFFFFu;
+  for (int i = 0; i < ITERS; ++i) a = sqr_r25(a);
+  out[blockIdx.x * 256 + threadIdx.x] = a.v[0] ^ a.v[9];
+  stamp(clk, t0, r0);
+}
+
+__global__ void k_check_r25(uint32_t* bad, uint32_t s) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  fe32 a = seed_fe32(s + t);
+  a.w[7] &= 0x7FFFFFFFu;
+  fe x = fe_from_words(a.w);
+  fe10 y = fe10_from_words(a.w);
+  for (int i = 0; i < 16; ++i) { y = sqr_r25(y); x = fe_sqr(x); }
+  uint32_t w[8], v[8];
+  fe10_to_words(y, w);
+  fe_to_words(x, v);
+  uint32_t diff = 0;
+  for (int i = 0; i < 8; ++i) diff |= w[i] ^ v[i];
+  if (diff) atomicAdd(bad, 1u);
+}
+
 typedef void (*kfn)(uint32_t*, unsigned long long*, uint32_t);
 
 // occupancy is pinned with dynamic LDS: w blocks of 256 lanes (one wave per SIMD each) per CU
@@ -248,6 +364,18 @@ int main() {
     printf("sqr_r32 vs fe_sqr: %u mismatches of %d (16 chained squarings each)\n", hb, 1024 * 256);
     CHK(hipFree(bad));
   }
+  {
+    uint32_t* bad;
+    CHK(hipMalloc(&bad, 4));
+    CHK(hipMemset(bad, 0, 4));
+    hipLaunchKernelGGL(k_check_r25, dim3(1024), dim3(256), 0, 0, bad, 777u);
+    uint32_t hb = 0;
+    CHK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
+    printf("sqr_r25 vs fe_sqr: %u mismatches of %d (16 chained squarings each)\n", hb, 1024 * 256);
+    CHK(hipFree(bad));
+  }
+  run("sqr_r25 w4", k_sqr_r25<4>, 4, ITERS, 0, d, clk, blocks);
+  run("sqr_r25 w8", k_sqr_r25<8>, 8, ITERS, 0, d, clk, blocks);
   run("sqr_r32 w4", k_sqr_r32<4>, 4, ITERS, 0, d, clk, blocks);
   run("sqr_r32 w8", k_sqr_r32<8>, 8, ITERS, 0, d, clk, blocks);
   run("mul w4", k_mul<4>, 4, ITERS, 456, d, clk, blocks);
