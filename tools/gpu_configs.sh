@@ -14,5 +14,11 @@ done
 # strong-scaling rehearsal of the multi-rank path: 2 ranks split ONE 2^20 batch, both on this GPU (gloo all-gather)
 EDC_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --scaling strong --steps 20 --warmup 3 > gpurun_out/${tag}_strong2_gloo.log 2>&1 || { echo strong_fail; tail -20 gpurun_out/${tag}_strong2_gloo.log; exit 1; }
 echo "strong2 $(grep '^{' gpurun_out/${tag}_strong2_gloo.log | tail -1 | cut -c1-300)"
+# weak-scaling rehearsal (the driver's default multi-GPU shape): 2 ranks, 2^20 each, both on this GPU
+EDC_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 20 --warmup 3 > gpurun_out/${tag}_weak2_gloo.log 2>&1 || { echo weak_fail; tail -20 gpurun_out/${tag}_weak2_gloo.log; exit 1; }
+echo "weak2 $(grep '^{' gpurun_out/${tag}_weak2_gloo.log | tail -1 | cut -c1-300)"
+# the shard size of a 2^20 batch over 8 GPUs, with the validator keys in the key cache (split coefficients)
+timeout -k 10 200 python -u bench.py --n 131072 --steps 40 --warmup 4 --inflight 8 --keycache --no-cpu-baseline > gpurun_out/${tag}_bench_n131072_keycache.log 2>&1 || { echo kc_fail; exit 1; }
+echo "n=131072 keycache $(tail -1 gpurun_out/${tag}_bench_n131072_keycache.log | cut -c1-200)"
 timeout -k 10 200 python -u tools/host_bench.py > gpurun_out/${tag}_host_bench.log 2>&1 || { echo host_fail; tail -5 gpurun_out/${tag}_host_bench.log; exit 1; }
 tail -3 gpurun_out/${tag}_host_bench.log
