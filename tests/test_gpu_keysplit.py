@@ -114,3 +114,53 @@ def test_split_in_flight_batches(cached, oracle_c):
         c8 = ctypes.create_string_buffer(32)
         rc = lib.edc_batch_wait(cached.ctx, t, c8, None, None)
         assert (rc, c8.raw) == exp
+
+
+@pytest.mark.parametrize("register", ["all", "validators"])
+def test_split_batch_then_grouped_fallback(cached, register):
+    """configs[3] shape on the split plan: the corpus, a forged signature, an undecodable key,
+    R and s; batch + grouped fallback in one call (which reuses the split batch's points and
+    sums) gives Item::verify_single's code for every item, twice in a row."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+    from conftest import golden
+    dev = torch.device("cuda:0")
+    L_ORDER = 2**252 + 27742317777372353535851937790883648493
+    rnd = random.Random(31337)
+    n, keys = 1 << 14, 150
+    vks, sigs, msgs = _batch(cached, rnd, n, keys)
+    validators = list(dict.fromkeys(vks))
+    expect = [0] * n
+    fx = golden("zip215_small_order.json")
+    pos = rnd.sample(range(n), len(fx["cases"]) + 4)
+    for p, c in zip(pos, fx["cases"]):
+        vks[p], sigs[p], msgs[p] = bytes.fromhex(c["vk"]), bytes.fromhex(c["sig"]), bytes.fromhex(fx["msg"])
+        expect[p] = c["expect_single"]
+    p_bad, p_A, p_R, p_s = pos[-4:]
+    msgs[p_bad] = msgs[p_bad][:-1] + bytes([msgs[p_bad][-1] ^ 1])
+    expect[p_bad] = 1
+    dec = [c for c in golden("decode.json")["cases"] if not c["ok"]]
+    vks[p_A] = bytes.fromhex(dec[0]["enc"])
+    expect[p_A] = 2
+    sigs[p_R] = bytes.fromhex(dec[1]["enc"]) + sigs[p_R][32:]
+    expect[p_R] = 1
+    s = int.from_bytes(sigs[p_s][32:], "little") + L_ORDER
+    sigs[p_s] = sigs[p_s][:32] + s.to_bytes(32, "little")
+    expect[p_s] = 1
+    cached.keycache_load(list(dict.fromkeys(vks)) if register == "all" else validators)
+    offs = [0]
+    for mm in msgs:
+        offs.append(offs[-1] + len(mm))
+
+    def _dev(b):
+        return torch.tensor(list(b) or [0], dtype=torch.uint8, device=dev)
+    d_vk, d_sig, d_msg = _dev(b"".join(vks)), _dev(b"".join(sigs)), _dev(b"".join(msgs))
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    for rep in range(2):
+        v = ctypes.create_string_buffer(n)
+        cnt = ctypes.c_int(-1)
+        rc = cached.lib.edc_batch_verify_fallback_device(cached.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(),
+                                                         d_msg.data_ptr(), d_off.data_ptr(), bytes([rep + 3]) * 32,
+                                                         v, ctypes.byref(cnt), None)
+        assert rc == 1 and cnt.value == 4 and list(v.raw) == expect, rep
