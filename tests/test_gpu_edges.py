@@ -137,3 +137,25 @@ def test_multi_more_devices_than_items_and_bad_args(edc, engine):
     assert lib.edc_set_msm_shape(engine.ctx, 12, 65) < 0
     assert lib.edc_set_fallback_shape(engine.ctx, 0, 10) < 0
     assert lib.edc_set_key_grouping(engine.ctx, 4) < 0
+
+
+def test_device_chacha_two_block_known_answer(engine):
+    """The device ChaCha20 (z stream, synthetic data) against the published zero-key blocks 0 and
+    1 of the original 64-bit-counter layout (rand_chacha's ChaCha20Rng), and a block past 2^32
+    against the oracle (the counter's high word)."""
+    torch = pytest.importorskip("torch")
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ed25519_ref as oracle
+    from test_oracle_golden import CHACHA20_ZERO_KEY_BLOCKS_0_1
+    dev = torch.device("cuda:0")
+    out = torch.zeros(128, dtype=torch.uint8, device=dev)
+    assert engine.lib.edc_chacha_fill_device(engine.ctx, bytes(32), 0, 2, out.data_ptr()) == 0
+    assert bytes(out.cpu().tolist()).hex() == CHACHA20_ZERO_KEY_BLOCKS_0_1
+    key = bytes(range(32))
+    blk = (1 << 32) + 5
+    assert engine.lib.edc_chacha_fill_device(engine.ctx, key, blk, 2, out.data_ptr()) == 0
+    assert bytes(out.cpu().tolist()) == oracle.chacha20_keystream(key, 128, blk)

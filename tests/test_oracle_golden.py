@@ -63,6 +63,29 @@ def test_decode_fixture_is_oracle_output(oracle):
             assert (pt[1] % oracle.P).to_bytes(32, "little").hex() == c["y"]
 
 
+# Published known answer for the original ChaCha20 layout (64-bit block counter in words 12-13,
+# 64-bit nonce in words 14-15 -- the layout of rand_chacha's ChaCha20Rng, which the reference's
+# z draws use, src/batch.rs:64-68 via rand_core 0.6): key = 0, nonce = 0, blocks 0 and 1
+# (draft-strombergson-chacha-test-vectors TC1, also rand_chacha's `test_chacha_true_values_a`
+# as u32 words 0xade0b876, 0x903df1a0, ... / 0xbee7079f, 0x7a385155, ...). Block 1 pins the
+# counter word the z stream advances, beyond the block-0 vector above.
+CHACHA20_ZERO_KEY_BLOCKS_0_1 = (
+    "76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+    "da41597c5157488d7724e03fb8d84a376a43b8f41518a11cc387b669b2ee6586"
+    "9f07e7be5551387a98ba977c732d080dcb0f29a048e3656912c6533e32ee7aed"
+    "29b721769ce64e43d57133b074d839d531ed1f28510afb45ace10a1f4b794d6f")
+
+
+def test_chacha_two_block_known_answer(oracle):
+    assert oracle.chacha20_keystream(bytes(32), 128).hex() == CHACHA20_ZERO_KEY_BLOCKS_0_1
+    # z_i = u128 of keystream bytes [16 i, 16 i + 16) little-endian (rand 0.8 Standard for u128:
+    # first next_u64 is the low half; BlockRng::next_u64 joins two u32 words low first)
+    z = oracle.z_values(bytes(32), 8)
+    ks = bytes.fromhex(CHACHA20_ZERO_KEY_BLOCKS_0_1)
+    assert z == [int.from_bytes(ks[16 * i:16 * i + 16], "little") for i in range(8)]
+    assert z[0] == 0x28bd8653e56a5d40903df1a0ade0b876
+
+
 def test_chacha_stream(oracle):
     fx = golden("chacha_z.json")
     # RFC 7539 2.3.2-style known answer: zero key, zero nonce, block 0
