@@ -505,6 +505,32 @@ __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_
   }
 }
 
+// Bin reduction for few bins (small batches, where it is latency): one workgroup per bin, its 64
+// quads run the cooperative weighted sum over the bin's 256 bucket sums (serial depth 26 quad
+// additions of 2 multiplication rounds each, instead of ~20 one-lane additions of 9 rounds).
+// About 4x the instructions of k_msm_reduce, so large batches keep the lane-parallel form.
+constexpr uint32_t REDUCE_QUAD_MAX_BINS = 128;
+__global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
+                                                         const uint32_t* __restrict__ buckets,
+                                                         uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t bin = blockIdx.x;
+  if (counts[bin] == 0) return;                     // the accumulation wrote W = T = 0
+  const int t = threadIdx.x;
+  st_ext(smem + t * EXT_WORDS, ld_ext(buckets + ((size_t)bin * NSLICE + t) * EXT_WORDS));
+  __syncthreads();
+  __builtin_amdgcn_s_setprio(3);
+  ge_p3 ws, tot;
+  weighted_sum_256(smem, smem, smem + 64 * EXT_WORDS, ws, tot);   // (sum_t t B_t, sum_t B_t)
+  if (t < 4) {
+    const ge_p3 W = quad_add(ws, tot);              // sum_t (t + 1) B_t
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+    }
+  }
+}
+
 // Win(range g, window w) = sum_s W_s + 256 * sum_s s T_s over the window's slices, for windows
 // with more than one slice (single-slice windows are read straight from their bin). One
 // workgroup per (range, window).
@@ -681,7 +707,9 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
                      buckets);
   hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
                      buckets, heads, slice_W, slice_T);
-  if (P.nbin() < 512)
+  if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
+    hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
+  else if (P.nbin() < 512)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
                        slice_T);
   else

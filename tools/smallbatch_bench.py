@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--sizes", default="8,16,24,32,40,48,56,64,150,1024")
+    ap.add_argument("--lib", default=None, help="A/B build of libedc.so (measurement only)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the batch's keys in the context's key cache first (a node's validator set)")
     args = ap.parse_args()
@@ -38,7 +39,7 @@ def main():
     dev = torch.device("cuda:0")
     torch.zeros(1, device=dev)
     pkg = bench.load_pkg()
-    eng = pkg.Engine(0)
+    eng = pkg.Engine(0, lib_path=args.lib)
     lib = eng.lib
     sizes = [int(x) for x in args.sizes.split(",")]
     nmax = max(sizes)
