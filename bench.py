@@ -384,6 +384,8 @@ def main():
             "hbm_view": ({"achieved_gbs": round(traffic / (dom_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
                           "frac": round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if traffic else None),
             "phases_ms": phases,
+            # one batch alone, start to verdict (sum of the phases of the instrumented batches)
+            "batch_latency_ms": round(sum(phases.values()), 3),
             "cpu_baseline": cpu,
             "gen_s": round(t_gen, 2),
         }
