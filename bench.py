@@ -188,7 +188,11 @@ def main():
     backend = os.environ.get("EDC_DIST_BACKEND", "nccl")
     if backend == "gloo":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    # EDC_FORCE_DIST=1 (rehearsal only): run the multi-rank path -- process group, per-batch
+    # all-gather of the 129-byte record, combine -- even for one rank, e.g. to exercise RCCL on a
+    # one-GPU box; the numbers are not a scaling measurement
+    force_dist = os.environ.get("EDC_FORCE_DIST") == "1"
+    if world > 1 or force_dist:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -223,7 +227,7 @@ def main():
         pending.append(t)
 
     def wait_oldest():
-        if world == 1:
+        if dist is None:
             rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
             return eng._check(rc)
         # multi-GPU: this rank's partial point of the global batch, all-gathered (RCCL) and combined

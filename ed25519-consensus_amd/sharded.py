@@ -33,16 +33,46 @@ def verify_sharded(partial_fn, combine_fn, allgather_fn, rank, world, n_local_ba
 
 
 def torch_allgather_fn(dist, device):
-    """all_gather of fixed 129-byte records over the default process group."""
+    """all_gather of fixed 129-byte records over the default process group.
+
+    On a GPU device every tensor op runs on a private non-blocking torch stream: the engine's
+    slot streams are blocking streams (hipExtStreamCreateWithCUMask takes no flags), so any work
+    on the legacy default stream would wait for -- and hold back -- every batch in flight. The
+    staging buffers are pinned and reused so the copies stay asynchronous DMA on that stream."""
+    import numpy as np
     import torch
+
+    if device.type == "cpu":
+        def fn_cpu(rec):
+            world = dist.get_world_size()
+            t = torch.frombuffer(bytearray(rec), dtype=torch.uint8)
+            out = torch.empty(world * len(rec), dtype=torch.uint8)
+            dist.all_gather_into_tensor(out, t)
+            host = out.numpy().tobytes()
+            return [host[i * len(rec):(i + 1) * len(rec)] for i in range(world)]
+        return fn_cpu
+
+    side = torch.cuda.Stream(device=device)
+    bufs = {}
 
     def fn(rec):
         world = dist.get_world_size()
-        t = torch.tensor(list(rec), dtype=torch.uint8, device=device)
-        out = torch.empty(world * len(rec), dtype=torch.uint8, device=device)
-        dist.all_gather_into_tensor(out, t)
-        host = out.cpu().numpy().tobytes()
-        return [host[i * len(rec):(i + 1) * len(rec)] for i in range(world)]
+        n = len(rec)
+        if n not in bufs:
+            with torch.cuda.stream(side):
+                bufs[n] = (torch.empty(n, dtype=torch.uint8, pin_memory=True),
+                           torch.empty(world * n, dtype=torch.uint8, pin_memory=True),
+                           torch.empty(n, dtype=torch.uint8, device=device),
+                           torch.empty(world * n, dtype=torch.uint8, device=device))
+        h_in, h_out, d_in, d_out = bufs[n]
+        with torch.cuda.stream(side):
+            h_in.numpy()[:] = np.frombuffer(rec, dtype=np.uint8)
+            d_in.copy_(h_in, non_blocking=True)
+            dist.all_gather_into_tensor(d_out, d_in)
+            h_out.copy_(d_out, non_blocking=True)
+            side.synchronize()
+            host = h_out.numpy().tobytes()
+        return [host[i * n:(i + 1) * n] for i in range(world)]
 
     return fn
 

@@ -42,11 +42,7 @@ def _worker(rank, world, port, name, out_path):
         part, bad = oracle_c.shard_partial_affine(items[lo:hi], seed, zbase)
         return part + bytes(64), bad          # pad the 64-byte affine record to 128
 
-    def allgather(rec):
-        t = torch.tensor(list(rec), dtype=torch.uint8)
-        out = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(out, t)
-        return [bytes(o.tolist()) for o in out]
+    allgather = sharded.torch_allgather_fn(dist, torch.device("cpu"))   # bench.py's gloo all-gather
 
     def combine(parts, bad_any):
         code, c8 = oracle_c.combine_affine([p[:64] for p in parts])
