@@ -227,27 +227,31 @@ def main():
         pending.append(t)
 
     def wait_oldest():
+        """Collect the oldest batch; returns a function that completes its verdict."""
         if dist is None:
-            rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
-            return eng._check(rc)
+            rc = eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None))
+            return lambda: rc
         # multi-GPU: this rank's partial point of the global batch, all-gathered (RCCL) and combined
         part = ctypes.create_string_buffer(128)
         bad = ctypes.c_int(0)
         eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, part, ctypes.byref(bad)))
-        code, _ = sharded.verify_sharded(lambda zb: (part.raw, bad.value), combine, allgather, rank, world, base)
-        return code
+        return lambda: sharded.verify_sharded(lambda zb: (part.raw, bad.value), combine, allgather, rank, world,
+                                              base)[0]
 
     def run_steps(k):
         """k full batch verifications; with --inflight F, batch i+F-1 is enqueued before batch i's
-        verdict is collected (every verdict is still waited for inside the loop). Multi-GPU: each
-        collected batch's partial point is all-gathered and combined while the later batches run."""
+        verdict is collected (every verdict is still completed inside the loop). Multi-GPU: the
+        freed slot is refilled first, then the collected batch's partial point is all-gathered and
+        combined while the later batches run (the exchange waits for GPU time on a full device;
+        the refill must not wait behind it)."""
         codes = []
         for _ in range(k):
-            if len(pending) >= max(1, args.inflight):
-                codes.append(wait_oldest())
+            done = wait_oldest() if len(pending) >= max(1, args.inflight) else None
             submit()
+            if done is not None:
+                codes.append(done())
         while pending:
-            codes.append(wait_oldest())
+            codes.append(wait_oldest()())
         return codes
 
     if args.keycache and args.keys > 0:           # a node's known validator set, registered once
