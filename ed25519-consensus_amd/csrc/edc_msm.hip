@@ -562,9 +562,9 @@ __global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* _
   __syncthreads();
   ge_p3 a = sum_256(sW, lpts);
   if (t < 4) {
-    ge_p3 x = ws;
-    for (int k = 0; k < SLICE_BITS; ++k) x = quad_dbl(x);
-    ge_p3 r = quad_add(a, x);
+    quad_pt x = quad_distribute(ws);
+    for (int k = 0; k < SLICE_BITS; ++k) x = quad_dbl_d(x);
+    ge_p3 r = quad_collect(quad_add_d(x, a));
     if (t == 0) st_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS, r);
   }
 }
@@ -627,12 +627,12 @@ __device__ __forceinline__ ge_p3 window_sum(const MsmPlan& P, uint32_t g, uint32
 
 // Horner over the windows of range g on one quad (4 cooperating lanes): sum_w 2^off[w] Win_w
 __device__ __forceinline__ ge_p3 horner(const MsmPlan& P, uint32_t g, const uint32_t* slice_W, const uint32_t* win) {
-  ge_p3 acc = window_sum(P, g, P.nwin - 1, slice_W, win);
+  quad_pt acc = quad_distribute(window_sum(P, g, P.nwin - 1, slice_W, win));
   for (int w = (int)P.nwin - 2; w >= 0; --w) {
-    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = quad_dbl(acc);
-    acc = quad_add(acc, window_sum(P, g, (uint32_t)w, slice_W, win));
+    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = quad_dbl_d(acc);
+    acc = quad_add_d(acc, window_sum(P, g, (uint32_t)w, slice_W, win));
   }
-  return acc;
+  return quad_collect(acc);
 }
 
 // batch: Horner, x8, identity (requires Z != 0), optional compression, partial point

@@ -101,7 +101,9 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t
     }
     return;
   }
-  const uint32_t j = i - n;
+  const uint32_t kbase = (n + 63u) & ~63u;   // key lanes start on a wave boundary (no R/key divergence)
+  if (i < kbase) return;
+  const uint32_t j = i - kbase;
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   if (j >= m) return;
   const bool per_sig = per_sig_host || flags[FLAG_OVF];
@@ -571,10 +573,16 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
                        const KeyCacheView& kc, bool split) {
-  // lanes [0, n) decode R_i, lanes [n, 2n) cover the largest possible key count (m <= n)
-  if (n)
-    hipLaunchKernelGGL(k_decompress, dim3(cdiv(2ull * n, 256)), dim3(256), 0, st, n, sig, vk, key_rep,
+  // lanes [0, n) decode R_i; the key lanes start at the next wave boundary and cover the largest
+  // possible key count (m <= n). A wave holding both would run both decodes one after the other,
+  // which doubles a small batch's decode latency. Small launches use one wave per workgroup so
+  // that the waves spread over CUs instead of sharing SIMDs.
+  if (n) {
+    const uint64_t lanes = ((n + 63ull) & ~63ull) + n;
+    const uint32_t block = lanes <= 16384 ? 64 : 256;
+    hipLaunchKernelGGL(k_decompress, dim3(cdiv(lanes, block)), dim3(block), 0, st, n, sig, vk, key_rep,
                        per_sig ? 1 : 0, pts, itembad, keybad, flags, kc, split ? 1 : 0);
+  }
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,

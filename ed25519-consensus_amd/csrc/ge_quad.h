@@ -120,4 +120,78 @@ __device__ __forceinline__ ge_p3 quad_add(const ge_p3& P, const ge_p3& Q) {
   return quad_add_cached(P, c);
 }
 
+// ---- distributed layout, for long serial chains (Horner, window combines) ----
+// Lane q of the quad holds ONE coordinate of the point (0: X, 1: Y, 2: Z, 3: T). The second
+// multiplication round of a doubling or addition then leaves each lane with exactly its own new
+// coordinate, so the final four-way broadcast of the replicated form (36 DPP moves) and the
+// four-way operand selects (27 v_cndmask each) disappear: every lane picks its operands from two
+// candidates under a fixed lane mask. Same formulas as quad_dbl / quad_add_cached, so every
+// coordinate is the same field element (the canonical bytes of a result are unchanged).
+struct quad_pt {
+  fe c;
+};
+
+__device__ __forceinline__ quad_pt quad_distribute(const ge_p3& P) {
+  return {quad_pick(quad_lane(), P.X, P.Y, P.Z, P.T)};
+}
+
+__device__ __forceinline__ ge_p3 quad_collect(const quad_pt& p) {
+  ge_p3 r;
+  quad_gather(p.c, r.X, r.Y, r.Z, r.T);
+  return r;
+}
+
+__device__ __forceinline__ fe fe_sel(bool c, const fe& a, const fe& b) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// 2P: lanes square X, Y, Z, (X+Y) (lane 3 drops T), then X3 = Xc Tc, Y3 = Yc Zc, Z3 = Zc Tc,
+// T3 = Xc Yc with a = (lane 1, 2 ? Zc : Xc) and b = (odd lane ? Yc : Tc)
+__device__ __forceinline__ quad_pt quad_dbl_d(const quad_pt& p) {
+  const int q = quad_lane();
+  fe x, y;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    x.v[i] = quad_bcast<0>(p.c.v[i]);
+    y.v[i] = quad_bcast<1>(p.c.v[i]);
+  }
+  const fe s = fe_sqr(fe_sel(q == 3, fe_add(x, y), p.c));
+  fe XX, YY, ZZ, XpY2;
+  quad_gather(s, XX, YY, ZZ, XpY2);
+  const fe ZZ2 = fe_add(ZZ, ZZ);
+  const fe Yc = fe_add(YY, XX);
+  const fe Zc = fe_sub(YY, XX);
+  const fe Xc = fe_sub(XpY2, Yc);
+  const fe Tc = fe_sub(ZZ2, Zc);
+  const bool mid = q == 1 || q == 2, odd = (q & 1) != 0;
+  return {fe_mul(fe_sel(mid, Zc, Xc), fe_sel(odd, Yc, Tc))};
+}
+
+// P + Q, Q extended and replicated on the quad's lanes: first round A = (Y1-X1)(Y2-X2),
+// B = (Y1+X1)(Y2+X2), lane 2 Z1 Z2, lane 3 T1 (2d T2); then X3 = E F, Y3 = G H, Z3 = F G,
+// T3 = E H with a = (lane 1, 2 ? G : E) and b = (odd lane ? H : F)
+__device__ __forceinline__ quad_pt quad_add_d(const quad_pt& p, const ge_p3& Q) {
+  const int q = quad_lane();
+  fe x, y;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    x.v[i] = quad_bcast<0>(p.c.v[i]);
+    y.v[i] = quad_bcast<1>(p.c.v[i]);
+  }
+  const fe qymx = fe_sub(Q.Y, Q.X), qypx = fe_add_c(Q.Y, Q.X);
+  const fe qt2d = fe_mul(Q.T, fe_d2());
+  const fe a = fe_sel(q == 0, fe_sub(y, x), fe_sel(q == 1, fe_add(y, x), p.c));
+  const fe b = fe_sel(q == 0, qymx, fe_sel(q == 1, qypx, fe_sel(q == 2, Q.Z, qt2d)));
+  const fe m = fe_mul(a, b);
+  fe A, B, ZZ, C;
+  quad_gather(m, A, B, ZZ, C);
+  const fe D = fe_add_c(ZZ, ZZ);
+  const fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  const bool mid = q == 1 || q == 2, odd = (q & 1) != 0;
+  return {fe_mul(fe_sel(mid, G, E), fe_sel(odd, H, F))};
+}
+
 }  // namespace edc
