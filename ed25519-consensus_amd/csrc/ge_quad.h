@@ -14,7 +14,7 @@ __device__ __forceinline__ int quad_lane() { return (int)(threadIdx.x & 3u); }
 
 template <int J>
 __device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J * 0x55, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, J * 0x55, 0xF, 0xF, true);
 }
 
 __device__ __forceinline__ void quad_gather(const fe& mine, fe& r0, fe& r1, fe& r2, fe& r3) {
@@ -149,7 +149,8 @@ __device__ __forceinline__ fe fe_sel(bool c, const fe& a, const fe& b) {
 }
 
 // 2P: lanes square X, Y, Z, (X+Y) (lane 3 drops T), then X3 = Xc Tc, Y3 = Yc Zc, Z3 = Zc Tc,
-// T3 = Xc Yc with a = (lane 1, 2 ? Zc : Xc) and b = (odd lane ? Yc : Tc)
+// T3 = Xc Yc (quad_dbl's completed-form values) with a = (lane 1, 2 ? Zc : Xc) and
+// b = (odd lane ? Yc : Tc)
 __device__ __forceinline__ quad_pt quad_dbl_d(const quad_pt& p) {
   const int q = quad_lane();
   fe x, y;
@@ -159,15 +160,21 @@ __device__ __forceinline__ quad_pt quad_dbl_d(const quad_pt& p) {
     y.v[i] = quad_bcast<1>(p.c.v[i]);
   }
   const fe s = fe_sqr(fe_sel(q == 3, fe_add(x, y), p.c));
-  fe XX, YY, ZZ, XpY2;
-  quad_gather(s, XX, YY, ZZ, XpY2);
-  const fe ZZ2 = fe_add(ZZ, ZZ);
-  const fe Yc = fe_add(YY, XX);
-  const fe Zc = fe_sub(YY, XX);
-  const fe Xc = fe_sub(XpY2, Yc);
-  const fe Tc = fe_sub(ZZ2, Zc);
+  // each lane forms only its two operands: a = u - v with u = (X+Y)^2 on lanes 0, 3 and Y^2 on
+  // lanes 1, 2 (one quad_perm [3,1,1,3] move per limb), v = Yc = Y^2 + X^2 or X^2, so a = Xc or
+  // Zc; b = X^2 + (odd lane ? Y^2 : 2Z^2 - Y^2), i.e. Yc or Tc = 2Z^2 - Zc
+  fe XX, YY, ZZ, u;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    XX.v[i] = quad_bcast<0>(s.v[i]);
+    YY.v[i] = quad_bcast<1>(s.v[i]);
+    ZZ.v[i] = quad_bcast<2>(s.v[i]);
+    u.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)s.v[i], 3 | (1 << 2) | (1 << 4) | (3 << 6), 0xF, 0xF, true);
+  }
   const bool mid = q == 1 || q == 2, odd = (q & 1) != 0;
-  return {fe_mul(fe_sel(mid, Zc, Xc), fe_sel(odd, Yc, Tc))};
+  const fe a = fe_sub(u, fe_sel(mid, XX, fe_add(YY, XX)));
+  const fe b = fe_add(XX, fe_sel(odd, YY, fe_sub(fe_add(ZZ, ZZ), YY)));
+  return {fe_mul(a, b)};
 }
 
 // P + Q, Q extended and replicated on the quad's lanes: first round A = (Y1-X1)(Y2-X2),
