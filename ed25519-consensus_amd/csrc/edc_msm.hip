@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
 //   returns (sum_t t * P_t, sum_t P_t), valid in quad 0 (threads 0..3).
 // Quad g folds points 4g..4g+3 (res_g = P1 + 2P2 + 3P3, run_g = sum), then a Hillis-Steele
 // suffix scan of run over the 64 quads gives sum_g 4g run_g = 4 sum_{g>=1} Suf_g; two trees
-// finish. Serial depth: 5 + 6 + 2*6 + 3 quad point ops. R and S are 64-point LDS scratch; they
+// finish (R on quads 0-31, S on quads 32-63). Serial depth: 5 + 6 + 6 + 3 quad point ops. R and S are 64-point LDS scratch; they
 // may alias lds_pts (every point is read before the first scratch write).
 __device__ __forceinline__ void weighted_sum_256(const uint32_t* lds_pts, uint32_t* R, uint32_t* S, ge_p3& wsum, ge_p3& tot) {
   const int g = threadIdx.x >> 2;
@@ -192,16 +192,17 @@ __device__ __forceinline__ void weighted_sum_256(const uint32_t* lds_pts, uint32
   if (g == 0) tot = ld_ext(S);
   __syncthreads();
   if (g == 0 && leader) st_ext(S, ge_identity());   // sum_{g>=1} Suf_g
-  // two trees: R (sum of res_g) and S (sum of suffixes), interleaved per step
+  // two trees at once: R (sum of res_g) on quads 0..31, S (sum of suffixes) on quads 32..63, so
+  // each level is one quad addition deep (waves 0-1 take R, waves 2-3 take S: no divergence)
+  const bool on_s = g >= 32;
+  const int h = on_s ? g - 32 : g;
+  uint32_t* const tree = on_s ? S : R;
   for (int d = 32; d >= 1; d >>= 1) {
     __syncthreads();
-    ge_p3 x, y;
-    if (g < d) {
-      x = quad_add(ld_ext(R + g * EXT_WORDS), ld_ext(R + (g + d) * EXT_WORDS));
-      y = quad_add(ld_ext(S + g * EXT_WORDS), ld_ext(S + (g + d) * EXT_WORDS));
-    }
+    ge_p3 x;
+    if (h < d) x = quad_add(ld_ext(tree + h * EXT_WORDS), ld_ext(tree + (h + d) * EXT_WORDS));
     __syncthreads();   // every lane reaches both barriers: none sits in a divergent branch
-    if (g < d && leader) { st_ext(R + g * EXT_WORDS, x); st_ext(S + g * EXT_WORDS, y); }
+    if (h < d && leader) st_ext(tree + h * EXT_WORDS, x);
   }
   __syncthreads();
   if (g == 0) wsum = quad_add(ld_ext(R), quad_dbl(quad_dbl(ld_ext(S))));
