@@ -117,13 +117,23 @@ __global__ void __launch_bounds__(1024) k_msm_scan(uint32_t nbin, const uint32_t
   }
 }
 
+// Scatter of every digit into its bin's run of `entries`. Pass 1 counts the workgroup's digits per
+// bin; each bin's run is reserved with one global atomic. Staged path (the workgroup's entries fit
+// its LDS stage, `stage_cap` > 0): pass 2 counting-sorts the entries by bin into the LDS stage
+// (bin kept in .y's upper bits), then the workgroup writes the stage out in order, so consecutive
+// lanes store consecutive entries of one run and every run leaves in whole-run wave stores
+// instead of one 8-byte store per digit spread over pass 2 (the scattered stores re-opened
+// partially written lines in L2: ~2.9x the entry bytes reached HBM). Direct path otherwise.
 __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint32_t per_block,
                                                      uint32_t* __restrict__ cursor, uint2* __restrict__ entries,
-                                                     const int* __restrict__ flags) {
+                                                     const int* __restrict__ flags, uint32_t stage_cap) {
   extern __shared__ uint32_t smem_hist[];
+  __shared__ uint32_t wsum[4];
   const uint32_t nbin = P.nbin();
   uint32_t* hist = smem_hist;
   uint32_t* gbase = smem_hist + nbin;
+  uint32_t* lbase = smem_hist + 2 * nbin;                                   // staged path only
+  uint2* stage = reinterpret_cast<uint2*>(smem_hist + 3 * nbin + (nbin & 1));  // 8-byte aligned
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   const uint32_t cnt = terms_count(T, flags);
@@ -138,10 +148,36 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) {
-    uint32_t c = hist[b];
+  // reserve each bin's run; staged path: exclusive scan of the counts over the bins (each lane
+  // takes a block of consecutive bins) into lbase, and the counters restart at lbase
+  const uint32_t per_lane = (nbin + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = min(nbin, threadIdx.x * per_lane), b1 = min(nbin, b0 + per_lane);
+  uint32_t mine = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = hist[b];
     gbase[b] = c ? atomicAdd(&cursor[b], c) : 0u;
-    hist[b] = 0;
+    mine += c;
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+    if (k < wave) before += wsum[k];
+    total += wsum[k];
+  }
+  const bool staged = total <= stage_cap;       // uniform over the workgroup
+  uint32_t run = before + incl - mine;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = hist[b];
+    if (staged) { lbase[b] = run; hist[b] = run; } else { hist[b] = 0; }
+    run += c;
   }
   __syncthreads();
   for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
@@ -152,8 +188,16 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     term_get(T, t, pt, rg, shrt, s);
     term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t local, bool neg) {
       const uint32_t r = atomicAdd(&hist[bin], 1u);
-      entries[gbase[bin] + r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local);
+      if (staged) stage[r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local | (bin << SLICE_BITS));
+      else entries[gbase[bin] + r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local);
     });
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const uint2 v = stage[e];
+    const uint32_t bin = v.y >> SLICE_BITS;
+    entries[gbase[bin] + (e - lbase[bin])] = make_uint2(v.x, v.y & (NSLICE - 1));
   }
 }
 
@@ -691,11 +735,25 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
   // at least ~256 workgroups so small batches still fill the GPU
   uint32_t per = max_terms / 256;
   per = per < 256 ? 256 : (per > 4096 ? 4096 : (per + 255) / 256 * 256);
+  // the scatter's LDS stage: what is left of 160 KB after three per-bin arrays, at most 16k
+  // entries; terms per workgroup then sized so that short-scalar workgroups fit it
+  const size_t lds_max = 160 * 1024 - 256, bins_bytes = (3 * (size_t)nbin + 1) * sizeof(uint32_t);
+  uint32_t stage_cap = bins_bytes + 2048 * sizeof(uint2) <= lds_max
+                           ? (uint32_t)std::min<size_t>(16384, (lds_max - bins_bytes) / sizeof(uint2) / 256 * 256)
+                           : 0u;
+  if (stage_cap) {
+    const uint32_t fit = stage_cap / std::max(1u, P.nwin_short) / 256 * 256;
+    if (fit >= 256 && per > fit) per = fit;
+  }
   const uint32_t grid = cdiv(max_terms ? max_terms : 1, per);
+  static const bool lds_attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msm_scatter),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)lds_max) == hipSuccess;
+  (void)lds_attr;
   hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
-  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), 2 * nbin * sizeof(uint32_t), st, P, T, per, cursor,
-                     entries, flags);
+  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), bins_bytes + (size_t)stage_cap * sizeof(uint2), st, P, T,
+                     per, cursor, entries, flags, stage_cap);
 }
 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
