@@ -15,6 +15,7 @@
 #include "edc_common.h"
 #include "edc_launch.h"
 #include "ge_quad.h"
+#include "ge_row.h"
 
 namespace edc {
 
@@ -606,11 +607,15 @@ __global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* _
   weighted_sum_256(lpts, lpts, lpts + 64 * EXT_WORDS, ws, tot);  // R/S scratch aliases the consumed points
   __syncthreads();
   ge_p3 a = sum_256(sW, lpts);
-  if (t < 4) {
-    quad_pt x = quad_distribute(ws);
-    for (int k = 0; k < SLICE_BITS; ++k) x = quad_dbl_d(x);
-    ge_p3 r = quad_collect(quad_add_d(x, a));
-    if (t == 0) st_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS, r);
+  __syncthreads();   // sum_256's last reads of lpts are done
+  if (t == 0) { st_ext(lpts, ws); st_ext(lpts + EXT_WORDS, a); }
+  __syncthreads();
+  if (t < 64) {      // 2^8 ws + a on wave 0's limb-sliced point (ge_row.h)
+    const RowCtx c = row_ctx();
+    const uint32_t bq = row_cached(c, lpts + EXT_WORDS, row_d2(c));
+    uint32_t x = row_ld_ext(c, lpts);
+    for (int k = 0; k < SLICE_BITS; ++k) x = row_dbl(c, x);
+    row_st_ext(c, win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS, row_add(c, x, bq));
   }
 }
 
@@ -664,30 +669,54 @@ __device__ void finish_point(const ge_p3& check, int bad, int want_compress, uin
 }
 
 // window sum of (range g, window w): combined by k_msm_window, or the single bin's W
-__device__ __forceinline__ ge_p3 window_sum(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* slice_W,
-                                             const uint32_t* win) {
-  if (P.nslice[w] * P.nsub[w] > 1 || P.sum_ranges) return ld_ext(win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS);
-  return ld_ext(slice_W + (size_t)(g * P.bins_per_range + P.bin0[w]) * EXT_WORDS);
+__device__ __forceinline__ const uint32_t* window_ptr(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* slice_W,
+                                                      const uint32_t* win) {
+  if (P.nslice[w] * P.nsub[w] > 1 || P.sum_ranges) return win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS;
+  return slice_W + (size_t)(g * P.bins_per_range + P.bin0[w]) * EXT_WORDS;
 }
 
-// Horner over the windows of range g on one quad (4 cooperating lanes): sum_w 2^off[w] Win_w
-__device__ __forceinline__ ge_p3 horner(const MsmPlan& P, uint32_t g, const uint32_t* slice_W, const uint32_t* win) {
-  quad_pt acc = quad_distribute(window_sum(P, g, P.nwin - 1, slice_W, win));
+// Horner over the windows of range g, sum_w 2^off[w] Win_w, on the wave's limb-sliced point
+// (ge_row.h: ~890 cycles per doubling against ~1980 on a quad). `cached` holds the second-operand
+// form of every window but the top one (row_cached, one word per lane, 64 words per window);
+// returns Win and [8]Win in `res` (two extended points, X | Y | Z | T).
+__device__ __forceinline__ void horner_row(const RowCtx& c, const MsmPlan& P, uint32_t g, const uint32_t* slice_W,
+                                           const uint32_t* win, const uint32_t* cached, uint32_t* res) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t acc = row_ld_ext(c, window_ptr(P, g, P.nwin - 1, slice_W, win));
   for (int w = (int)P.nwin - 2; w >= 0; --w) {
-    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = quad_dbl_d(acc);
-    acc = quad_add_d(acc, window_sum(P, g, (uint32_t)w, slice_W, win));
+    const uint32_t bq = cached[w * 64 + lane];
+    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = row_dbl(c, acc);
+    acc = row_add(c, acc, bq);
   }
-  return quad_collect(acc);
+  row_st_ext(c, res, acc);
+  acc = row_dbl(c, row_dbl(c, row_dbl(c, acc)));
+  row_st_ext(c, res + EXT_WORDS, acc);
 }
 
-// batch: Horner, x8, identity (requires Z != 0), optional compression, partial point
-__global__ void k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W, const uint32_t* __restrict__ win,
-                            const int* __restrict__ flags, int want_compress, uint8_t* __restrict__ out) {
-  if (threadIdx.x >= 4 || blockIdx.x != 0) return;
+// second-operand forms of range g's windows 0..nwin-2 into cached[] by the workgroup's `nwave` waves
+__device__ __forceinline__ void cache_windows(const RowCtx& c, const MsmPlan& P, uint32_t g, const uint32_t* slice_W,
+                                              const uint32_t* win, uint32_t* cached, uint32_t wave, uint32_t nwave) {
+  const uint32_t d2 = row_d2(c), lane = threadIdx.x & 63;
+  for (uint32_t w = wave; w + 1 < P.nwin; w += nwave) cached[w * 64 + lane] = row_cached(c, window_ptr(P, g, w, slice_W, win), d2);
+}
+
+// batch: Horner, x8, identity (requires Z != 0), optional compression, partial point. Four waves
+// form the windows' addition operands, then wave 0 runs the serial chain.
+__global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
+                                                   const uint32_t* __restrict__ win, const int* __restrict__ flags,
+                                                   int want_compress, uint8_t* __restrict__ out) {
+  __shared__ uint32_t cached[MSM_MAX_WIN * 64];
+  __shared__ uint32_t res[2 * EXT_WORDS];
+  if (blockIdx.x != 0) return;
   __builtin_amdgcn_s_setprio(3);   // a serial chain: issue ahead of co-resident bulk waves
-  const ge_p3 acc = horner(P, 0, slice_W, win);
-  ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
+  const RowCtx c = row_ctx();
+  const uint32_t wave = threadIdx.x >> 6;
+  cache_windows(c, P, 0, slice_W, win, cached, wave, 4);
+  __syncthreads();
+  if (wave == 0) horner_row(c, P, 0, slice_W, win, cached, res);
+  __syncthreads();
   if (threadIdx.x != 0) return;
+  const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
   ext_to_canonical_bytes(acc, out + 48);
   const int bad = flags[FLAG_BAD];
   reinterpret_cast<int*>(out)[0] = (!bad && ge_is_identity(c8)) ? 0 : 1;
@@ -703,16 +732,20 @@ __global__ void k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W, con
   }
 }
 
-// ranges: rverdict[g] = 0 iff [8] * (range g's check point) is the identity; one quad per range
+// ranges: rverdict[g] = 0 iff [8] * (range g's check point) is the identity; one wave per range
 __global__ void __launch_bounds__(64) k_msm_range_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
                                                         const uint32_t* __restrict__ win,
                                                         uint8_t* __restrict__ rverdict) {
-  const uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;   // a quad never straddles the bound
+  __shared__ uint32_t cached[MSM_MAX_WIN * 64];
+  __shared__ uint32_t res[2 * EXT_WORDS];
+  const uint32_t g = blockIdx.x;
   if (g >= P.nranges) return;
   __builtin_amdgcn_s_setprio(3);
-  const ge_p3 acc = horner(P, g, slice_W, win);
-  const ge_p3 c8 = quad_dbl(quad_dbl(quad_dbl(acc)));
-  if ((threadIdx.x & 3) == 0) rverdict[g] = ge_is_identity(c8) ? 0 : 1;
+  const RowCtx c = row_ctx();
+  cache_windows(c, P, g, slice_W, win, cached, 0, 1);
+  horner_row(c, P, g, slice_W, win, cached, res);
+  __syncthreads();
+  if (threadIdx.x == 0) rverdict[g] = ge_is_identity(ld_ext(res + EXT_WORDS)) ? 0 : 1;
 }
 
 // combine G partial check points (canonical 128-byte records) from G shards
@@ -795,15 +828,14 @@ void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, 
                      uint32_t* win, int* flags, int want_compress, uint8_t* out) {
   if (plan_multi(P) || P.sum_ranges)
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(64), 0, st, P, slice_W, win, flags, want_compress, out);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out);
 }
 
 void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                            uint32_t* win, uint8_t* rverdict) {
   if (plan_multi(P))
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin * P.nranges), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
-  hipLaunchKernelGGL(k_msm_range_final, dim3(cdiv(4ull * P.nranges, 64)), dim3(64), 0, st, P, slice_W, win,
-                     rverdict);
+  hipLaunchKernelGGL(k_msm_range_final, dim3(P.nranges), dim3(64), 0, st, P, slice_W, win, rverdict);
 }
 
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
