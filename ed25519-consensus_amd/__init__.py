@@ -2,7 +2,7 @@
 
 The reference (informalsystems/ed25519-consensus 2.1.0) is Rust; no Rust toolchain exists in
 this image, so the host side above the C ABI (include/edc.h, built as csrc/libedc.so) is this
-module plus the C++ header csrc/edc.hpp. Names, argument meaning and error behaviour follow the
+module (the Rust binding a maintainer would add is in INTEGRATION.md). Names, argument meaning and error behaviour follow the
 reference:
 
     reference                                   here
@@ -45,6 +45,7 @@ ABI_SYMBOLS = [
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
+    "edc_multi_submit", "edc_multi_submit_device", "edc_multi_wait", "edc_set_slots",
 ]
 
 
@@ -131,6 +132,13 @@ def load_library(path=None):
         lib.edc_multi_batch_verify.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp]
         lib.edc_multi_batch_verify_fallback.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, c_vp,
                                                         ctypes.POINTER(ctypes.c_int), c_vp]
+        lib.edc_multi_submit.restype = ctypes.c_int64
+        lib.edc_multi_submit.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_u8p, ctypes.c_int]
+        lib.edc_multi_submit_device.restype = ctypes.c_int64
+        lib.edc_multi_submit_device.argtypes = [c_vp, ctypes.POINTER(c_sz), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
+                                                ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_u8p, ctypes.c_int]
+        lib.edc_multi_wait.argtypes = [c_vp, ctypes.c_int64, c_vp]
+        lib.edc_set_slots.argtypes = [c_vp, ctypes.c_int]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_decompress.argtypes = [c_vp, c_sz, c_u8p, c_vp, c_vp]
@@ -377,6 +385,7 @@ class MultiEngine:
             raise EngineError(f"edc_create_multi({list(devices)}) failed")
         self.devices = list(devices)
         self._lock = threading.Lock()
+        self._inflight = {}
 
     def close(self):
         if self.m:
@@ -400,6 +409,38 @@ class MultiEngine:
         with self._lock:
             rc = self.lib.edc_multi_batch_verify(self.m, len(vks), b"".join(vks) or b"\0", b"".join(sigs) or b"\0",
                                                  arena, offs, bytes(z_seed), check8)
+        self._check(rc)
+        return rc, (check8.raw if check8 is not None else None)
+
+    def batch_submit(self, vks, sigs, msgs, z_seed, want_check8=False):
+        """Pipelined multi-device batch (edc_multi_submit): returns a ticket; the host buffers are
+        kept alive here until batch_wait(ticket)."""
+        arena, offs = _arena(msgs)
+        bufs = (b"".join(vks) or b"\0", b"".join(sigs) or b"\0", arena, offs, bytes(z_seed))
+        with self._lock:
+            t = self.lib.edc_multi_submit(self.m, len(vks), bufs[0], bufs[1], bufs[2], bufs[3], bufs[4],
+                                          1 if want_check8 else 0)
+            self._check(t)
+            self._inflight[t] = bufs
+        return t
+
+    def batch_submit_device(self, shards, z_seed, want_check8=False):
+        """edc_multi_submit_device: shards[g] = (n, d_vk, d_sig, d_msg, d_msg_off) as device pointers
+        (ints) on device g; returns a ticket."""
+        G = len(shards)
+        n = (ctypes.c_size_t * G)(*[s[0] for s in shards])
+        ptr = lambda k: (ctypes.c_void_p * G)(*[s[k] for s in shards])
+        with self._lock:
+            t = self.lib.edc_multi_submit_device(self.m, n, ptr(1), ptr(2), ptr(3), ptr(4), bytes(z_seed),
+                                                 1 if want_check8 else 0)
+            self._check(t)
+        return t
+
+    def batch_wait(self, ticket, want_check8=False):
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            rc = self.lib.edc_multi_wait(self.m, ticket, check8)
+            self._inflight.pop(ticket, None)
         self._check(rc)
         return rc, (check8.raw if check8 is not None else None)
 

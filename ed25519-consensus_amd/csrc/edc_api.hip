@@ -27,7 +27,10 @@ hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, count * sizeof(T));
 }
 
-constexpr int kSlots = 8;  // batches that can be in flight per context
+#ifndef EDC_SLOTS
+#define EDC_SLOTS 8
+#endif
+constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
 }  // namespace
@@ -90,6 +93,7 @@ struct edc_ctx {
   float last_ms[PH_N] = {};
   int nlast = 0;
   int64_t next_ticket = 0;
+  int nslots = kSlots;          // in-flight slots the submissions rotate over (edc_set_slots)
   // adaptive key grouping (edc_set_key_grouping): mode 0 = auto, 1 = always group, 2 = never
   int key_grouping = 0;
   bool have_key_ratio = false;  // a grouped batch has completed on this context
@@ -666,7 +670,7 @@ edc_ctx* edc_create(int device) {
     ctx->secret = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
   }
   (void)hipGetLastError();   // launch checks below must not see an earlier, unrelated failure
-  bool ok = hipSetDevice(device) == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
+  bool ok = hipSetDevice(device) == hipSuccess && msm_init_device() == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
             dalloc(&ctx->btab, BTAB_ENTRIES * NIELS_WORDS) == hipSuccess;
   if (ok) {
     launch_init_btable(ctx->st(), ctx->btab);
@@ -771,7 +775,7 @@ int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, con
   if (!ctx || (!z_seed && !d_z)) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
   const int64_t ticket = ctx->next_ticket;
-  Slot& s = ctx->slot[ticket % kSlots];
+  Slot& s = ctx->slot[ticket % ctx->nslots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, d_z, want_check8 != 0);
   if (rc) return rc;
@@ -785,7 +789,7 @@ int64_t edc_batch_submit(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_
   if (!ctx || !z_seed) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
   const int64_t ticket = ctx->next_ticket;
-  Slot& s = ctx->slot[ticket % kSlots];
+  Slot& s = ctx->slot[ticket % ctx->nslots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = upload_slot(ctx, s, n, vk, sig, msg, msg_off);
   if (rc) return rc;
@@ -805,7 +809,7 @@ int64_t edc_batch_submit_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx
   for (size_t i = 0; i < n; ++i) mx = key_idx[i] > mx ? key_idx[i] : mx;
   if (n && mx >= ctx->kc_reg_m) { ctx->err = "key index outside the registered key list"; return EDC_ERR_ARG; }
   const int64_t ticket = ctx->next_ticket;
-  Slot& s = ctx->slot[ticket % kSlots];
+  Slot& s = ctx->slot[ticket % ctx->nslots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = upload_slot(ctx, s, n, nullptr, sig, msg, msg_off, key_idx);
   if (rc) return rc;
@@ -819,7 +823,7 @@ int64_t edc_batch_submit_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx
 int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad) {
   if (!ctx || ticket < 0) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  Slot& s = ctx->slot[ticket % kSlots];
+  Slot& s = ctx->slot[ticket % ctx->nslots];
   if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
   return finish_batch(ctx, s, check8, partial, bad);
 }
@@ -928,7 +932,7 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
   return 0;
 }
 
-// ---- grouped fallback: one MSM pass over ~256 contiguous ranges ----
+// ---- grouped fallback: one MSM pass over ~32 contiguous ranges (edc_set_fallback_shape) ----
 static int ensure_fb(edc_ctx* ctx, size_t terms, size_t ranges) {
   if (terms > ctx->fb_cap_terms || !ctx->fb_xpt) {
     CK(hipStreamSynchronize(ctx->st()));
@@ -986,8 +990,8 @@ static int verify_listed(edc_ctx* ctx, Slot& s, const std::vector<uint32_t>& idx
 }
 
 // After a failed batch on slot s (its k, decoded points, key grouping and per-item failure bits
-// still in place): the batch equation restricted to ~256 contiguous ranges in ONE MSM pass
-// (range-tagged bins, 9-bit windows), [8]P_g == 0 per range; ranges whose check fails or that
+// still in place): the batch equation restricted to ~fb_ranges (default 32) contiguous ranges in
+// ONE MSM pass (range-tagged bins, fb_bits = 10-bit windows by default), [8]P_g == 0 per range; ranges whose check fails or that
 // hold an item with an undecodable R / key or a non-canonical s are verified item by item.
 // Items of passing ranges are valid (ZIP215: batch == single, with a fresh secret z: see
 // include/edc.h). verdicts (host, n bytes) receive Item::verify_single's code for every item.
@@ -999,7 +1003,11 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   // ~FB_RANGES ranges: each range-window bin then holds enough digits to amortize its fixed
   // 256-bucket reduction, and a failing range costs no more than a small one in the per-item pass
   // (that pass is latency-bound: one lane per item)
-  const size_t target = (n + ctx->fb_ranges - 1) / ctx->fb_ranges;
+  // the range count is capped so that the range-tagged plan fits MSM_MAX_BINS (G * bins per range)
+  const uint32_t bpr = make_plan(ctx->fb_bits, ctx->fb_bits, 1).bins_per_range;
+  const uint32_t gmax = MSM_MAX_BINS / bpr;
+  const uint32_t granges = ctx->fb_ranges < gmax ? ctx->fb_ranges : gmax;
+  const size_t target = (n + granges - 1) / granges;
   const size_t rsize = (target + COEF_CHUNK - 1) / COEF_CHUNK * COEF_CHUNK;
   const uint32_t G = (uint32_t)((n + rsize - 1) / rsize);
   if (!per_sig && (size_t)G * m > s.cap_n) {
@@ -1256,6 +1264,15 @@ int edc_chacha_fill_device(edc_ctx* ctx, const uint8_t key[32], uint64_t blk0, u
   return 0;
 }
 
+int edc_set_slots(edc_ctx* ctx, int k) {
+  if (!ctx || k < 1 || k > kSlots) return EDC_ERR_ARG;
+  for (Slot& s : ctx->slot)
+    if (s.pending) { ctx->err = "slot count change with a batch in flight"; return EDC_ERR_ARG; }
+  ctx->nslots = k;
+  ctx->next_ticket = 0;
+  return 0;
+}
+
 int edc_set_key_grouping(edc_ctx* ctx, int mode) {
   if (!ctx || mode < 0 || mode > 3) return EDC_ERR_ARG;
   ctx->key_grouping = mode;
@@ -1301,7 +1318,8 @@ int edc_reserve(edc_ctx* ctx, size_t n) {
   size_t e1 = msm_entry_capacity(dense, n, n + 1), e2 = msm_entry_capacity(few, n, n + 1);
   const size_t e3 = msm_entry_capacity(splitp, 2 + 3 * n, 0);   // split coefficients (key cache)
   if (e3 > e1) e1 = e3;
-  for (Slot& s : ctx->slot) {
+  for (int i = 0; i < ctx->nslots; ++i) {
+    Slot& s = ctx->slot[i];
     if (s.pending) { ctx->err = "reserve with a batch in flight"; return EDC_ERR_ARG; }
     int rc = ensure_slot(ctx, s, n);
     if (rc) return rc;
@@ -1342,9 +1360,29 @@ int edc_synchronize(edc_ctx* ctx) {
 // partials are gathered through the host (they already come back with each shard's verdict) and
 // summed on the first device, then x8 and the identity test. One host thread per device drives
 // its shard; the same device may appear several times (several contexts on one GPU).
+// One in-flight multi-device batch (edc_multi_submit): every shard's 256-byte result block is
+// copied device to device (a peer store over xGMI by a one-wave kernel on the shard's stream; a
+// plain copy when a device is listed twice) into
+// `blocks` on the first device, whose combine stream waits for every shard's copy event and sums
+// the partial points there (k_combine_blocks). The host only enqueues, and waits once per batch.
+struct MultiSlot {
+  bool pending = false;
+  int64_t ticket = -1;
+  bool want = false;
+  std::vector<int64_t> shard;        // shard tickets, one per context
+  std::vector<hipEvent_t> copied;    // recorded on each shard's slot stream after its block copy
+  hipEvent_t done = nullptr;         // first device, after the combine
+  uint8_t* blocks = nullptr;         // first device: ndev x 256 bytes
+  uint8_t* d_out = nullptr;          // first device: 256-byte verdict block
+  uint8_t* h_out = nullptr;          // pinned mirror
+};
+
 struct edc_multi {
   std::vector<edc_ctx*> ctx;
   std::string err;
+  MultiSlot ms[kSlots];
+  int64_t next_ticket = 0;
+  hipStream_t comb = nullptr;        // first device: every batch's combine, in submission order
 };
 
 struct Shard {
@@ -1402,6 +1440,87 @@ static int multi_batch(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t*
   return rc;
 }
 
+#define MCK(expr)                                                       \
+  do {                                                                  \
+    hipError_t e_ = (expr);                                             \
+    if (e_ != hipSuccess) {                                             \
+      (void)hipGetLastError();                                          \
+      M->err = std::string(#expr) + ": " + hipGetErrorString(e_);       \
+      return EDC_ERR_HIP;                                               \
+    }                                                                   \
+  } while (0)
+
+static int multi_slot_init(edc_multi* M, MultiSlot& ms) {
+  if (ms.done) return 0;
+  const size_t g = M->ctx.size();
+  MCK(hipSetDevice(M->ctx[0]->device));
+  // the combines are tiny and in order: one ordinary stream for all of them (the shard contexts'
+  // slot streams already hold a hardware queue each)
+  if (!M->comb) MCK(hipStreamCreateWithFlags(&M->comb, hipStreamNonBlocking));
+  MCK(hipEventCreateWithFlags(&ms.done, hipEventDisableTiming));
+  MCK(hipMalloc((void**)&ms.blocks, 256 * g));
+  MCK(hipMalloc((void**)&ms.d_out, 256));
+  MCK(hipHostMalloc((void**)&ms.h_out, 256));
+  ms.copied.assign(g, nullptr);
+  for (size_t i = 0; i < g; ++i) {
+    MCK(hipSetDevice(M->ctx[i]->device));
+    MCK(hipEventCreateWithFlags(&ms.copied[i], hipEventDisableTiming));
+  }
+  return 0;
+}
+
+static void multi_slot_free(edc_multi* M, MultiSlot& ms) {
+  if (!ms.done) return;
+  (void)hipSetDevice(M->ctx[0]->device);
+  (void)hipEventSynchronize(ms.done);
+  for (hipEvent_t e : ms.copied)
+    if (e) (void)hipEventDestroy(e);
+  if (ms.done) (void)hipEventDestroy(ms.done);
+  if (ms.blocks) (void)hipFree(ms.blocks);
+  if (ms.d_out) (void)hipFree(ms.d_out);
+  if (ms.h_out) (void)hipHostFree(ms.h_out);
+  ms = MultiSlot();
+}
+
+// After shard g's batch was enqueued on its context (ticket t): copy its result block to the first
+// device behind the batch, on the shard's slot stream, and let the combine stream wait for it.
+static int multi_link_shard(edc_multi* M, MultiSlot& ms, size_t g, int64_t t) {
+  edc_ctx* c = M->ctx[g];
+  Slot& s = c->slot[t % c->nslots];
+  if (!s.pending || s.ticket != t || !s.d_out) { M->err = "shard ticket has no pending slot"; return EDC_ERR_ARG; }
+  MCK(hipSetDevice(c->device));
+  launch_copy_block(s.st, s.d_out, ms.blocks + 256 * g);   // hipMemcpyPeerAsync blocks the host here
+  MCK(hipGetLastError());
+  MCK(hipEventRecord(ms.copied[g], s.st));
+  MCK(hipSetDevice(M->ctx[0]->device));
+  MCK(hipStreamWaitEvent(M->comb, ms.copied[g], 0));
+  return 0;
+}
+
+// enqueue the combine of every shard's block on the first device; the batch is then in flight
+static int multi_finish_submit(edc_multi* M, MultiSlot& ms, int64_t ticket, int want_check8) {
+  MCK(hipSetDevice(M->ctx[0]->device));
+  launch_combine_blocks(M->comb, (uint32_t)M->ctx.size(), ms.blocks, want_check8 != 0, ms.d_out);
+  MCK(hipGetLastError());
+  MCK(hipMemcpyAsync(ms.h_out, ms.d_out, 256, hipMemcpyDeviceToHost, M->comb));
+  MCK(hipEventRecord(ms.done, M->comb));
+  ms.pending = true;
+  ms.ticket = ticket;
+  ms.want = want_check8 != 0;
+  M->next_ticket++;
+  return ticket >= 0 ? 0 : EDC_ERR_ARG;
+}
+
+// shard g's submission failed after earlier shards were enqueued: drain those so that their
+// contexts' tickets stay consistent, and report the failure
+static int multi_abort(edc_multi* M, MultiSlot& ms, size_t failed, bool link_failed, int rc) {
+  const std::string why = link_failed ? M->err : std::string(edc_last_error(M->ctx[failed]));
+  for (size_t g = 0; g < ms.shard.size(); ++g)
+    if (ms.shard[g] >= 0) (void)edc_batch_wait(M->ctx[g], ms.shard[g], nullptr, nullptr, nullptr);
+  M->err = std::string("device ") + std::to_string(M->ctx[failed]->device) + ": " + why;
+  return rc < 0 ? rc : EDC_ERR_ARG;
+}
+
 extern "C" {
 
 edc_multi* edc_create_multi(const int* devices, int ndev) {
@@ -1415,13 +1534,108 @@ edc_multi* edc_create_multi(const int* devices, int ndev) {
     }
     M->ctx.push_back(c);
   }
+  // contexts sharing one GPU split its eight in-flight slots (one hardware queue each), so that a
+  // rehearsal with a device listed several times does not oversubscribe the queue scheduler
+  for (int i = 0; i < ndev; ++i) {
+    int same = 0;
+    for (int j = 0; j < ndev; ++j) same += devices[j] == devices[i];
+    M->ctx[i]->nslots = kSlots / same > 0 ? kSlots / same : 1;
+  }
+  // direct xGMI copies of the shards' result blocks to the first device (edc_multi_submit)
+  for (int i = 1; i < ndev; ++i) {
+    if (devices[i] == devices[0]) continue;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, devices[0], devices[i]) == hipSuccess && can) {
+      (void)hipSetDevice(devices[i]);
+      (void)hipDeviceEnablePeerAccess(devices[0], 0);   // already enabled is fine
+      (void)hipGetLastError();
+    }
+  }
   return M;
 }
 
 void edc_destroy_multi(edc_multi* M) {
   if (!M) return;
+  for (MultiSlot& ms : M->ms) multi_slot_free(M, ms);
+  if (M->comb) {
+    (void)hipSetDevice(M->ctx[0]->device);
+    (void)hipStreamDestroy(M->comb);
+  }
   for (edc_ctx* c : M->ctx) edc_destroy(c);
   delete M;
+}
+
+int64_t edc_multi_submit(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t z_seed[32], int want_check8) {
+  if (!M || !z_seed || (n && (!vk || !sig || !msg_off))) return EDC_ERR_ARG;
+  const int64_t ticket = M->next_ticket;
+  MultiSlot& ms = M->ms[ticket % kSlots];
+  if (ms.pending) { M->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = multi_slot_init(M, ms);
+  if (rc) return rc;
+  std::vector<Shard> sh;
+  shard_bounds(n, M->ctx.size(), sh);
+  ms.shard.assign(sh.size(), -1);
+  for (size_t g = 0; g < sh.size(); ++g) {
+    const size_t lo = sh[g].lo, m = sh[g].hi - lo;
+    const int64_t t = edc_batch_submit(M->ctx[g], m, vk + 32 * lo, sig + 64 * lo, msg, msg_off + lo, z_seed, lo, 0);
+    if (t < 0) return multi_abort(M, ms, g, false, (int)t);
+    ms.shard[g] = t;
+    rc = multi_link_shard(M, ms, g, t);
+    if (rc) return multi_abort(M, ms, g, true, rc);
+  }
+  rc = multi_finish_submit(M, ms, ticket, want_check8);
+  return rc ? rc : ticket;
+}
+
+int64_t edc_multi_submit_device(edc_multi* M, const size_t* n, const uint8_t* const* d_vk, const uint8_t* const* d_sig,
+                                const uint8_t* const* d_msg, const uint64_t* const* d_msg_off,
+                                const uint8_t z_seed[32], int want_check8) {
+  if (!M || !z_seed || !n || !d_vk || !d_sig || !d_msg || !d_msg_off) return EDC_ERR_ARG;
+  const int64_t ticket = M->next_ticket;
+  MultiSlot& ms = M->ms[ticket % kSlots];
+  if (ms.pending) { M->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = multi_slot_init(M, ms);
+  if (rc) return rc;
+  const size_t G = M->ctx.size();
+  ms.shard.assign(G, -1);
+  uint64_t base = 0;
+  for (size_t g = 0; g < G; ++g) {
+    const int64_t t = edc_batch_submit_device(M->ctx[g], n[g], d_vk[g], d_sig[g], d_msg[g], d_msg_off[g], z_seed,
+                                              base, nullptr, 0);
+    if (t < 0) return multi_abort(M, ms, g, false, (int)t);
+    ms.shard[g] = t;
+    rc = multi_link_shard(M, ms, g, t);
+    if (rc) return multi_abort(M, ms, g, true, rc);
+    base += n[g];
+  }
+  rc = multi_finish_submit(M, ms, ticket, want_check8);
+  return rc ? rc : ticket;
+}
+
+int edc_multi_wait(edc_multi* M, int64_t ticket, uint8_t check8[32]) {
+  if (!M || ticket < 0) return EDC_ERR_ARG;
+  MultiSlot& ms = M->ms[ticket % kSlots];
+  if (!ms.pending || ms.ticket != ticket) { M->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
+  ms.pending = false;
+  int err = 0;
+  for (size_t g = 0; g < ms.shard.size(); ++g) {   // retire the shard tickets (grouping statistics)
+    const int r = edc_batch_wait(M->ctx[g], ms.shard[g], nullptr, nullptr, nullptr);
+    if (r < 0 && !err) {
+      err = r;
+      M->err = std::string("device ") + std::to_string(M->ctx[g]->device) + ": " + edc_last_error(M->ctx[g]);
+    }
+  }
+  if (err) return err;
+  MCK(hipSetDevice(M->ctx[0]->device));
+  MCK(hipEventSynchronize(ms.done));
+  const int verdict = reinterpret_cast<int*>(ms.h_out)[0];
+  const int bad = reinterpret_cast<int*>(ms.h_out)[1];
+  if (check8) {
+    if (bad || !ms.want) memset(check8, 0, 32);
+    else memcpy(check8, ms.h_out + 16, 32);
+  }
+  return verdict ? EDC_INVALID_SIGNATURE : EDC_OK;
 }
 
 int edc_multi_size(const edc_multi* M) { return M ? (int)M->ctx.size() : 0; }

@@ -39,6 +39,9 @@ void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, con
 // block, table[0..T) = 0xFFFFFFFF, counts[0..nbin) = 0 (T / nbin may be 0)
 void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long* u_acc, uint8_t* d_out, uint32_t* table,
                        uint32_t T, uint32_t* counts, uint32_t nbin);
+// edc_msm.hip: per-device kernel attributes (the scatter's dynamic LDS beyond 64 KB); call on
+// every device a context uses, after hipSetDevice
+hipError_t msm_init_device();
 // edc_msm.hip (counts_zeroed: the caller already cleared counts, e.g. launch_init_batch)
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed = false);
@@ -52,6 +55,10 @@ void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* sli
                            uint32_t* win, uint8_t* rverdict);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
                     uint8_t* out);
+// 256-byte result block src -> dst (dst may be a peer device's memory)
+void launch_copy_block(hipStream_t st, const uint8_t* src, uint8_t* dst);
+// g shard result blocks (256 bytes each, device) -> verdict block (as launch_combine)
+void launch_combine_blocks(hipStream_t st, uint32_t g, const uint8_t* blocks, int want_compress, uint8_t* out);
 size_t msm_entry_capacity(const MsmPlan& P, size_t short_terms, size_t full_terms);
 // edc_single.hip
 void launch_init_btable(hipStream_t st, uint32_t* btab);

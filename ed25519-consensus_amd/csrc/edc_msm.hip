@@ -757,8 +757,30 @@ __global__ void k_combine(uint32_t g, const uint8_t* __restrict__ partials, int 
   finish_point(acc, bad, want_compress, out);
 }
 
+// combine the result blocks of g shards (256-byte blocks: int[1] bad flag, bytes 48..176 the
+// canonical partial point), as the pipelined multi-device path gathers them device to device
+__global__ void k_combine_blocks(uint32_t g, const uint8_t* __restrict__ blocks, int want_compress,
+                                 uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 acc = ge_identity();
+  int bad = 0;
+  for (uint32_t i = 0; i < g; ++i) {
+    acc = ge_add(acc, ext_from_canonical_bytes(blocks + 256 * (size_t)i + 48));
+    bad |= reinterpret_cast<const int*>(blocks + 256 * (size_t)i)[1];
+  }
+  for (int j = 0; j < 64; ++j) reinterpret_cast<int*>(out)[j] = 0;
+  finish_point(acc, bad, want_compress, out);
+}
+
+// one shard's 256-byte result block to the first device's gather buffer (a peer store over xGMI
+// when the devices differ): a kernel on the shard's stream, so the copy stays asynchronous
+__global__ void k_copy_block(const uint4* __restrict__ src, uint4* __restrict__ dst) {
+  if (threadIdx.x < 16) dst[threadIdx.x] = src[threadIdx.x];
+}
+
 // ---------------------------------------------------------------- launchers
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+static constexpr size_t kScatterLdsMax = 160 * 1024 - 256;   // k_msm_scatter's dynamic LDS ceiling
 
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed) {
@@ -770,7 +792,7 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
   per = per < 256 ? 256 : (per > 4096 ? 4096 : (per + 255) / 256 * 256);
   // the scatter's LDS stage: what is left of 160 KB after three per-bin arrays, at most 16k
   // entries; terms per workgroup then sized so that short-scalar workgroups fit it
-  const size_t lds_max = 160 * 1024 - 256, bins_bytes = (3 * (size_t)nbin + 1) * sizeof(uint32_t);
+  const size_t lds_max = kScatterLdsMax, bins_bytes = (3 * (size_t)nbin + 1) * sizeof(uint32_t);
   uint32_t stage_cap = bins_bytes + 2048 * sizeof(uint2) <= lds_max
                            ? (uint32_t)std::min<size_t>(16384, (lds_max - bins_bytes) / sizeof(uint2) / 256 * 256)
                            : 0u;
@@ -779,14 +801,15 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
     if (fit >= 256 && per > fit) per = fit;
   }
   const uint32_t grid = cdiv(max_terms ? max_terms : 1, per);
-  static const bool lds_attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msm_scatter),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   (int)lds_max) == hipSuccess;
-  (void)lds_attr;
   hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
   hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), bins_bytes + (size_t)stage_cap * sizeof(uint2), st, P, T,
                      per, cursor, entries, flags, stage_cap);
+}
+
+hipError_t msm_init_device() {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msm_scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)kScatterLdsMax);
 }
 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
@@ -836,6 +859,15 @@ void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* sli
   if (plan_multi(P))
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin * P.nranges), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
   hipLaunchKernelGGL(k_msm_range_final, dim3(P.nranges), dim3(64), 0, st, P, slice_W, win, rverdict);
+}
+
+void launch_copy_block(hipStream_t st, const uint8_t* src, uint8_t* dst) {
+  hipLaunchKernelGGL(k_copy_block, dim3(1), dim3(64), 0, st, reinterpret_cast<const uint4*>(src),
+                     reinterpret_cast<uint4*>(dst));
+}
+
+void launch_combine_blocks(hipStream_t st, uint32_t g, const uint8_t* blocks, int want_compress, uint8_t* out) {
+  hipLaunchKernelGGL(k_combine_blocks, dim3(1), dim3(64), 0, st, g, blocks, want_compress, out);
 }
 
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,

@@ -145,8 +145,9 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
 /*
  * Grouped fallback after a failed batch (the caller-driven Item::verify_single loop of
  * reference tests/batch.rs:37-43, src/batch.rs:104-107). The batch equation is linear, so it
- * restricts to any subset of the items: ONE range-tagged MSM pass evaluates it over ~256
- * contiguous ranges (same z, same k, the decoded points of the batch prefix); ranges whose
+ * restricts to any subset of the items: ONE range-tagged MSM pass evaluates it over about 32
+ * contiguous ranges by default (edc_set_fallback_shape; same z, same k, the decoded points of the
+ * batch prefix); ranges whose
  * [8]*check is not the identity, or that hold an item with an undecodable R / key or a
  * non-canonical s, are verified item by item. verdicts (host, n bytes) receive
  * Item::verify_single's code for every item. Returns the number of invalid items, or <0.
@@ -277,10 +278,18 @@ int edc_set_msm_bin_entries(edc_ctx* ctx, int entries);
 
 /*
  * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous
- * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). Results never depend
- * on it.
+ * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). The range count is
+ * capped so that ranges x bins per range stays within the MSM's 8192 bins (e.g. at most 24 ranges
+ * with 13-bit windows). Results never depend on it.
  */
 int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits);
+
+/*
+ * Number of in-flight slots (1..8, default 8) this context's submissions rotate over; each slot
+ * holds its own workspace and hardware queue. Contexts that share one GPU (edc_create_multi with
+ * a repeated device) get 8 / (contexts on that GPU). Refused while batches are in flight.
+ */
+int edc_set_slots(edc_ctx* ctx, int k);
 
 /*
  * Pre-allocate the workspaces of every in-flight slot for batches of up to n items (otherwise
@@ -307,7 +316,8 @@ int edc_synchronize(edc_ctx* ctx);
  * draws its z at its global queue indices, evaluates its part of the batch equation to one
  * partial point (128 bytes); the partials are gathered through the host and combined on the
  * first device (x8, identity). Verdicts and check8 are bit-identical to edc_batch_verify on one
- * device for any device list. Host buffers as edc_batch_verify; synchronous.
+ * device for any device list. Host buffers as edc_batch_verify; synchronous (the pipelined,
+ * device-to-device form is edc_multi_submit / edc_multi_wait below).
  */
 typedef struct edc_multi edc_multi;
 edc_multi* edc_create_multi(const int* devices, int ndev);
@@ -318,6 +328,27 @@ edc_ctx* edc_multi_context(edc_multi* m, int i);
 const char* edc_multi_last_error(const edc_multi* m);
 int edc_multi_batch_verify(edc_multi* m, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                            const uint64_t* msg_off, const uint8_t z_seed[32], uint8_t check8[32]);
+/*
+ * Pipelined form of edc_multi_batch_verify for a node verifying block after block across its
+ * GPUs (reference src/batch.rs:149-217, one Verifier::verify per block): edc_multi_submit splits
+ * the batch into contiguous shards, enqueues each on its device's next in-flight slot (host
+ * inputs copied on that slot's stream, as edc_batch_submit) and returns a ticket >= 0 without
+ * waiting. Each shard's 128-byte partial point (with its bad flag) is copied device to device to
+ * the first device (peer copy over xGMI), where a combine on its own stream sums the partials
+ * (x8, identity) as soon as the last shard lands. edc_multi_wait blocks for the ticket and
+ * returns EDC_OK / EDC_INVALID_SIGNATURE / <0 with optional check8 (needs want_check8). Up to 8
+ * batches in flight; tickets are waited in submission order; host buffers are borrowed until the
+ * wait. edc_multi_submit_device takes per-device slices already resident in each device's HBM:
+ * n[g] items at d_vk[g], d_sig[g], d_msg[g], d_msg_off[g] form shard g, with global queue indices
+ * (for z) starting at n[0] + ... + n[g-1]. Verdicts and check8 equal edc_batch_verify of the
+ * concatenated batch on one device.
+ */
+int64_t edc_multi_submit(edc_multi* m, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t z_seed[32], int want_check8);
+int64_t edc_multi_submit_device(edc_multi* m, const size_t* n, const uint8_t* const* d_vk,
+                                const uint8_t* const* d_sig, const uint8_t* const* d_msg,
+                                const uint64_t* const* d_msg_off, const uint8_t z_seed[32], int want_check8);
+int edc_multi_wait(edc_multi* m, int64_t ticket, uint8_t check8[32]);
 /*
  * edc_multi_batch_verify and, on failure, the grouped fallback on every shard whose own partial
  * fails (edc_batch_verify_fallback_device semantics): verdicts (host, n bytes) = Item::verify_single

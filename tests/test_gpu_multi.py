@@ -68,3 +68,75 @@ def test_multi_config3_scale(multi, engine):
     code, c8 = multi.batch_verify([vks[i] for i in keep], [sigs[i] for i in keep], [msgs[i] for i in keep], zs,
                                   want_check8=True)
     assert code == 0 and c8 == IDENTITY
+
+
+@pytest.mark.parametrize("b", golden("batches.json")["batches"], ids=lambda b: b["name"])
+def test_multi_submit_fixture(multi, b):
+    """Pipelined multi-device form (edc_multi_submit / edc_multi_wait: shard partials copied
+    device to device and combined on the first device): every golden batch, submitted twice and
+    in flight together, gives the fixture's verdict and [8]*check."""
+    it = _items(b)
+    vks, sigs, msgs = [v for v, _, _ in it], [s for _, s, _ in it], [m for _, _, m in it]
+    zs = bytes.fromhex(b["z_seed"])
+    t1 = multi.batch_submit(vks, sigs, msgs, zs, want_check8=True)
+    t2 = multi.batch_submit(vks, sigs, msgs, zs, want_check8=True)
+    for t in (t1, t2):
+        code, c8 = multi.batch_wait(t, want_check8=True)
+        assert code == b["expect_code"]
+        if b["expect_check8"] is not None:
+            assert c8.hex() == b["expect_check8"]
+
+
+def test_multi_submit_device_config3(multi, engine):
+    """Device-resident pipelined form (edc_multi_submit_device) on configs[3] at 2^20: per-device
+    slices of one batch (the ZIP215 corpus + one bad signature among 2^20 votes) -> Err, and the
+    same batch without the bad item -> Ok with the identity, several batches in flight."""
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    fx = golden("zip215_small_order.json")
+    pkg = sys.modules["ed25519_consensus_amd"]
+    vk, sig, msg, off, expect, _ = bench.make_c4_workload(pkg, engine, torch, dev, n, 150, 120, fx["cases"],
+                                                          bytes.fromhex(fx["msg"]))
+    G = len(multi.devices)
+
+    def shards(vk, sig, msg, off, n):
+        out = []
+        for g in range(G):
+            lo, hi = n * g // G, n * (g + 1) // G
+            o = (off[lo:hi + 1] - off[lo]).contiguous()
+            keep.append(o)
+            out.append((hi - lo, vk.data_ptr() + 32 * lo, sig.data_ptr() + 64 * lo,
+                        msg.data_ptr() + int(off[lo].item()), o.data_ptr()))
+        return out
+
+    keep = []
+    zs = bytes([0x33]) * 32
+    t_bad = multi.batch_submit_device(shards(vk, sig, msg, off, n), zs, want_check8=True)
+    # the batch without every item whose verify_single fails (re-packed on the device)
+    idx = torch.tensor([i for i in range(n) if i not in expect], dtype=torch.int64, device=dev)
+    vk2 = vk.view(-1, 32)[:n][idx].reshape(-1).contiguous()
+    sig2 = sig.view(-1, 64)[:n][idx].reshape(-1).contiguous()
+    lens = (off[1:] - off[:-1])[idx]
+    off2 = torch.zeros(len(idx) + 1, dtype=torch.int64, device=dev)
+    off2[1:] = torch.cumsum(lens, 0)
+    cols = torch.arange(int(lens.max().item()), device=dev)[None, :]
+    starts = off[:-1][idx]
+    msg2 = torch.cat([msg[(starts[:, None] + cols)[cols < lens[:, None]]], torch.zeros(1, dtype=torch.uint8, device=dev)])
+    n2 = len(idx)
+    # two batches in flight per context at most (contexts sharing one GPU split its 8 slots)
+    sh2 = shards(vk2, sig2, msg2, off2, n2)
+    t_ok = [multi.batch_submit_device(sh2, zs, want_check8=True)]
+    code, _ = multi.batch_wait(t_bad, want_check8=True)
+    assert code == 1
+    t_ok.append(multi.batch_submit_device(sh2, zs, want_check8=True))
+    for t in t_ok:
+        code, c8 = multi.batch_wait(t, want_check8=True)
+        assert code == 0 and c8 == IDENTITY
+    # single-device reference of the same cleaned batch: same verdict
+    rc = engine.lib.edc_batch_verify_device(engine.ctx, n2, vk2.data_ptr(), sig2.data_ptr(), msg2.data_ptr(),
+                                            off2.data_ptr(), zs, 0, None, None)
+    assert rc == 0
+
