@@ -142,6 +142,31 @@ def cpu_baseline(vk, sig, msg, off, n_sample, keys, msg_len):
     return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len, data=data)
 
 
+def openssl_anchor(seconds=2, cores=1):
+    """SURVEY.md 8(d) / BASELINE.md anchor: `openssl speed ed25519` verify/s on the host. OpenSSL
+    verifies one signature at a time under RFC 8032 cofactorless rules (it rejects non-canonical
+    encodings and small-order keys that ZIP215 accepts), so it is a CPU scale reference for the
+    primitive, not a parity baseline. Runs the system binary; None when it is absent."""
+    import re
+    import shutil
+    import subprocess
+    exe = shutil.which("openssl")
+    if exe is None:
+        return None
+    cmd = [exe, "speed", "-seconds", str(seconds)] + (["-multi", str(cores)] if cores > 1 else []) + ["ed25519"]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=20 * seconds + 30, cwd="/tmp").stdout
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "sample": f"openssl speed failed: {e}"}
+    m = re.search(r"Ed25519\)\s+\S+\s+\S+\s+([0-9.]+)\s+([0-9.]+)", out)
+    if m is None:
+        return {"value": None, "sample": "openssl speed output not parsed"}
+    ver = out.strip().splitlines()[0] if out.strip() else "openssl"
+    return {"value": float(m.group(2)), "unit": "verify/s", "cores": cores, "kind": "openssl speed ed25519",
+            "rules": "RFC 8032 single verify (cofactorless, canonical encodings only), not ZIP215 batch",
+            "sample": f"{' '.join(cmd[1:])} ({ver})"}
+
+
 CONFIGS = {   # BASELINE.json configs: (items per GPU, validators (0 = distinct keys), message bytes (-1 = 0..1024))
     "c2": (1 << 16, 0, 32, "configs[1]: 2^16 sigs, distinct keys, 32-byte msgs"),
     "c3": (1 << 20, 150, 120, "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs"),
@@ -352,6 +377,8 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
             cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
+            if isinstance(cpu, dict):
+                cpu["openssl_anchor"] = openssl_anchor()
         alg_sig = ALG_MAD_PER_SIG_REPEATED if args.keys > 0 else ALG_MAD_PER_SIG_DISTINCT
         line = {
             "metric": "Ed25519 batch-verified signatures/sec (whole node) at 2^20 sigs",
