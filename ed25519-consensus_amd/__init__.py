@@ -45,7 +45,7 @@ ABI_SYMBOLS = [
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
-    "edc_multi_submit", "edc_multi_submit_device", "edc_multi_wait", "edc_set_slots",
+    "edc_multi_submit", "edc_multi_submit_device", "edc_multi_wait", "edc_set_slots", "edc_debug_set_scatter_stage",
 ]
 
 
@@ -120,6 +120,8 @@ def load_library(path=None):
                                                          ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_set_msm_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
         lib.edc_set_msm_bin_entries.argtypes = [c_vp, ctypes.c_int]
+        if hasattr(lib, "edc_debug_set_scatter_stage"):      # absent from older A/B builds (tools/)
+            lib.edc_debug_set_scatter_stage.argtypes = [ctypes.c_uint32]
         lib.edc_set_fallback_shape.argtypes = [c_vp, ctypes.c_int, ctypes.c_int]
         lib.edc_create_multi.restype = c_vp
         lib.edc_create_multi.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]

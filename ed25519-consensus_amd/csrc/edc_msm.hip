@@ -125,11 +125,42 @@ __global__ void __launch_bounds__(1024) k_msm_scan(uint32_t nbin, const uint32_t
 // lanes store consecutive entries of one run and every run leaves in whole-run wave stores
 // instead of one 8-byte store per digit spread over pass 2 (the scattered stores re-opened
 // partially written lines in L2: ~2.9x the entry bytes reached HBM). Direct path otherwise.
-__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint32_t per_block,
+// Workgroup -> terms of the scatter. Batches with full-width terms use two regions, so that every
+// workgroup's entries fit the LDS stage: region A holds the short terms 1..n (R_i, nwin_short
+// digits each) at per_a terms per workgroup; region B the full-width terms (B, then the keys:
+// term 0 and terms n+1.., all windows) at per_b = per_a * nwin_short / nwin. One region
+// (grid_a = grid, a0 = 0) otherwise. Term t of a workgroup is its u-th: region A t = a0 + base + u
+// (t < a_end); region B v = base + u, t = v ? b_base + v : 0.
+struct ScatterBlocks {
+  uint32_t grid_a, per_a, a0, a_end, per_b, b_base;
+};
+template <typename F>
+__device__ __forceinline__ void scatter_terms(const ScatterBlocks& S, uint32_t cnt, F&& f) {
+  if (blockIdx.x < S.grid_a) {
+    const uint32_t t0 = S.a0 + blockIdx.x * S.per_a, lim = min(cnt, S.a_end);
+    for (uint32_t u = threadIdx.x; u < S.per_a; u += blockDim.x) {
+      if (t0 + u >= lim) break;
+      f(t0 + u);
+    }
+  } else {
+    const uint32_t v0 = (blockIdx.x - S.grid_a) * S.per_b;
+    for (uint32_t u = threadIdx.x; u < S.per_b; u += blockDim.x) {
+      const uint32_t v = v0 + u, t = v ? S.b_base + v : 0u;
+      if (t >= cnt) break;
+      f(t);
+    }
+  }
+}
+
+#ifndef EDC_SCATTER_THREADS
+#define EDC_SCATTER_THREADS 1024
+#endif
+constexpr int SCATTER_THREADS = EDC_SCATTER_THREADS;
+__global__ void __launch_bounds__(SCATTER_THREADS) k_msm_scatter(MsmPlan P, MsmTerms T, ScatterBlocks SB,
                                                      uint32_t* __restrict__ cursor, uint2* __restrict__ entries,
                                                      const int* __restrict__ flags, uint32_t stage_cap) {
   extern __shared__ uint32_t smem_hist[];
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t wsum[SCATTER_THREADS / 64];
   const uint32_t nbin = P.nbin();
   uint32_t* hist = smem_hist;
   uint32_t* gbase = smem_hist + nbin;
@@ -138,16 +169,13 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   const uint32_t cnt = terms_count(T, flags);
-  const uint32_t t0 = blockIdx.x * per_block;
   // pass 1: local counts (recomputed in pass 2 from the same digits)
-  for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
-    const uint32_t t = t0 + u;
-    if (t >= cnt) break;
+  scatter_terms(SB, cnt, [&](uint32_t t) {
     uint32_t pt, rg, s[8];
     bool shrt;
     term_get(T, t, pt, rg, shrt, s);
     term_digits(P, t, shrt, rg, s, [&](uint32_t bin, uint32_t, bool) { atomicAdd(&hist[bin], 1u); });
-  }
+  });
   __syncthreads();
   // reserve each bin's run; staged path: exclusive scan of the counts over the bins (each lane
   // takes a block of consecutive bins) into lbase, and the counters restart at lbase
@@ -181,9 +209,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
     run += c;
   }
   __syncthreads();
-  for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
-    const uint32_t t = t0 + u;
-    if (t >= cnt) break;
+  scatter_terms(SB, cnt, [&](uint32_t t) {
     uint32_t pt, rg, s[8];
     bool shrt;
     term_get(T, t, pt, rg, shrt, s);
@@ -192,7 +218,7 @@ __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan P, MsmTerms T, uint
       if (staged) stage[r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local | (bin << SLICE_BITS));
       else entries[gbase[bin] + r] = make_uint2(pt | (neg ? 0x80000000u : 0u), local);
     });
-  }
+  });
   if (!staged) return;
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < total; e += blockDim.x) {
@@ -556,6 +582,10 @@ __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_
 // additions of 2 multiplication rounds each, instead of ~20 one-lane additions of 9 rounds).
 // About 4x the instructions of k_msm_reduce, so large batches keep the lane-parallel form.
 constexpr uint32_t REDUCE_QUAD_MAX_BINS = 128;
+#ifndef EDC_REDUCE64_MAX_BINS
+#define EDC_REDUCE64_MAX_BINS 512
+#endif
+constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per bin below this many bins
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ buckets,
                                                          uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
@@ -781,6 +811,13 @@ __global__ void k_copy_block(const uint4* __restrict__ src, uint4* __restrict__ 
 // ---------------------------------------------------------------- launchers
 static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
 static constexpr size_t kScatterLdsMax = 160 * 1024 - 256;   // k_msm_scatter's dynamic LDS ceiling
+// entries of the scatter's LDS stage (process-wide; edc_debug_set_scatter_stage lowers it so that
+// tests can drive the direct-store path, which the default stage covers only at large bin counts)
+static uint32_t g_scatter_stage_max = 16384;
+extern "C" int edc_debug_set_scatter_stage(uint32_t max_entries) {
+  g_scatter_stage_max = max_entries > 16384 ? 16384u : max_entries;
+  return 0;
+}
 
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed) {
@@ -791,20 +828,34 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
   uint32_t per = max_terms / 256;
   per = per < 256 ? 256 : (per > 4096 ? 4096 : (per + 255) / 256 * 256);
   // the scatter's LDS stage: what is left of 160 KB after three per-bin arrays, at most 16k
-  // entries; terms per workgroup then sized so that short-scalar workgroups fit it
+  // entries; terms per workgroup then sized so that every workgroup's digits fit it (ScatterBlocks)
   const size_t lds_max = kScatterLdsMax, bins_bytes = (3 * (size_t)nbin + 1) * sizeof(uint32_t);
   uint32_t stage_cap = bins_bytes + 2048 * sizeof(uint2) <= lds_max
-                           ? (uint32_t)std::min<size_t>(16384, (lds_max - bins_bytes) / sizeof(uint2) / 256 * 256)
+                           ? (uint32_t)std::min<size_t>(g_scatter_stage_max, (lds_max - bins_bytes) / sizeof(uint2) / 256 * 256)
                            : 0u;
-  if (stage_cap) {
-    const uint32_t fit = stage_cap / std::max(1u, P.nwin_short) / 256 * 256;
-    if (fit >= 256 && per > fit) per = fit;
-  }
   const uint32_t grid = cdiv(max_terms ? max_terms : 1, per);
+  ScatterBlocks SB{grid, per, 0u, 0xFFFFFFFFu, per, 0u};
+  uint32_t sgrid = grid;
+  if (stage_cap) {
+    const auto fit = [&](uint32_t digits) { return stage_cap / std::max(1u, digits) / 256 * 256; };
+    const uint32_t fa = fit(P.nwin_short), fb = fit(P.nwin);
+    if (!T.rsize && !T.split && P.nwin > P.nwin_short && fa >= 256 && fb >= 256) {   // batch: short region, then full-width
+      SB.per_a = std::min(per, fa);
+      SB.per_b = std::min(per, fb);
+      SB.a0 = 1;
+      SB.a_end = 1 + T.n;
+      SB.b_base = T.n;
+      SB.grid_a = cdiv(T.n ? T.n : 1, SB.per_a);
+      sgrid = SB.grid_a + cdiv(max_terms > T.n ? max_terms - T.n : 1, SB.per_b);
+    } else if (fa >= 256 && per > fa) {
+      SB.per_a = SB.per_b = fa;
+      SB.grid_a = sgrid = cdiv(max_terms ? max_terms : 1, fa);
+    }
+  }
   hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
-  hipLaunchKernelGGL(k_msm_scatter, dim3(grid), dim3(256), bins_bytes + (size_t)stage_cap * sizeof(uint2), st, P, T,
-                     per, cursor, entries, flags, stage_cap);
+  hipLaunchKernelGGL(k_msm_scatter, dim3(sgrid), dim3(SCATTER_THREADS), bins_bytes + (size_t)stage_cap * sizeof(uint2), st, P, T,
+                     SB, cursor, entries, flags, stage_cap);
 }
 
 hipError_t msm_init_device() {
@@ -824,7 +875,7 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
                      buckets, heads, slice_W, slice_T);
   if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
-  else if (P.nbin() < 512)
+  else if (P.nbin() < REDUCE64_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
                        slice_T);
   else

@@ -277,6 +277,13 @@ int edc_set_msm_shape(edc_ctx* ctx, int bits, int parts);
 int edc_set_msm_bin_entries(edc_ctx* ctx, int entries);
 
 /*
+ * Test knob (process-wide): at most `max_entries` (0..16384, default 16384) MSM entries per
+ * workgroup go through the binning scatter's LDS stage; workgroups with more store each entry
+ * directly. 0 forces the direct stores everywhere. Results never depend on it.
+ */
+int edc_debug_set_scatter_stage(uint32_t max_entries);
+
+/*
  * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous
  * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). The range count is
  * capped so that ranges x bins per range stays within the MSM's 8192 bins (e.g. at most 24 ranges

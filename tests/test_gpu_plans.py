@@ -67,3 +67,23 @@ def test_grouping_modes_and_overflow_path(engine, oracle_c, mode, m, bad):
     finally:
         engine.set_key_grouping(0)
     assert (code, c8) == (exp_code, exp_c8)
+
+
+@pytest.mark.parametrize("stage", [0, 512])
+@pytest.mark.parametrize("n,m,bad", [(4096, 256, 77), (8192, 150, None), (6000, 6000, 17)])
+@pytest.mark.parametrize("bits,parts", [(0, 0), (16, 1), (11, 16)])
+def test_scatter_direct_path_matches_oracle(engine, oracle_c, stage, n, m, bad, bits, parts):
+    """The binning scatter's direct-store path (workgroups whose digits overflow the LDS stage:
+    at the default 16k-entry stage only very large bin counts take it) and a small stage that
+    splits workgroups between both paths, against the C oracle (that path was only
+    covered by bench.py's valid-batch assert)."""
+    vks, sigs, msgs, zseed = _batch(engine, n, m, bad, seed=stage + 7)
+    exp_code, exp_c8 = oracle_c.batch_verify(list(zip(vks, sigs, msgs)), zseed)
+    engine.lib.edc_debug_set_scatter_stage(stage)
+    engine.set_msm_shape(bits, parts)
+    try:
+        for _ in range(2):
+            assert engine.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True) == (exp_code, exp_c8)
+    finally:
+        engine.set_msm_shape(0, 0)
+        engine.lib.edc_debug_set_scatter_stage(16384)
