@@ -187,7 +187,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
-    ap.add_argument("--inflight", type=int, default=6, help="batches in flight per GPU (submit/wait pipelining, <= 8)")
+    ap.add_argument("--inflight", type=int, default=6, help="batches in flight per GPU (submit/wait pipelining, <= the build's slot count, 8)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",

@@ -28,9 +28,18 @@ hipError_t dalloc(T** p, size_t count) {
 }
 
 #ifndef EDC_SLOTS
-#define EDC_SLOTS 8
+#define EDC_SLOTS 16
 #endif
 constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
+// Timing probes only (make variant VFLAGS=-DEDC_PROBE_SKIP=<mask>, tools/phase_cost.sh): after a
+// slot's first batch, skip a phase's launches (its outputs stay from that batch, which the bench
+// repeats), to measure what the phase costs inside the pipeline: 2 SHA-512, 4 coefficients,
+// 8 binning, 16 decompression, 32 accumulation, 64 bin reduction, 128 window combine + Horner,
+// 256 bucket sort. The product build has mask 0.
+#ifndef EDC_PROBE_SKIP
+#define EDC_PROBE_SKIP 0
+#endif
+#define EDC_RUN(bit) ((EDC_PROBE_SKIP & (bit)) == 0 || s.probe_runs == 0)
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
 }  // namespace
@@ -70,6 +79,7 @@ struct Slot {
   bool per_sig = false;         // this batch skipped key grouping (adaptive grouping)
   uint32_t n_batch = 0;
   int64_t ticket = -1;
+  uint32_t probe_runs = 0;      // batches enqueued (EDC_PROBE_SKIP timing builds only)
 };
 
 struct edc_ctx {
@@ -563,7 +573,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   s.n_batch = N;
   mark(PH_KEYS);
   launch_init_batch(st, s.flags, per_sig ? (int)N : -1, s.u_acc, s.d_out, per_sig ? nullptr : s.table, per_sig ? 0u : T,
-                    with_bin ? s.counts : nullptr, with_bin ? P->nbin() : 0u);
+                    with_bin && EDC_RUN(8) ? s.counts : nullptr, with_bin && EDC_RUN(8) ? P->nbin() : 0u);
   if (!per_sig) {
     const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
     const uint32_t salt[2] = {(uint32_t)h, (uint32_t)(h >> 32)};
@@ -571,18 +581,18 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
                 s.key_index, s.key_acc, s.flags);
   }
   mark(PH_CHALLENGE);
-  launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
+  if (EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
-  launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
+  if (EDC_RUN(4)) launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
               per_sig, s.coef_part, split);
   mark(PH_MSM_BIN);
-  if (with_bin)
+  if (with_bin && EDC_RUN(8))
     launch_msm_bin(st, *P, batch_terms(*P, s, N, split), split ? 2 + 3 * N : 1 + 2 * N, s.counts, s.offsets, s.cursor,
                    s.entries, s.flags, true);
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
-  launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc(), split);
+  if (EDC_RUN(16)) launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc(), split);
   CK(hipGetLastError());
   return 0;
 }
@@ -603,13 +613,14 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
-                    s.slice_T);
+                    s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0);
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
-  launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out);
+  // the final kernel stores the result block to d_out and straight into the pinned h_out
+  if (EDC_RUN(128)) launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out, s.h_out);
   if (s.timed) (void)hipEventRecord(s.ev[PH_N], st);
   CK(hipGetLastError());
-  CK(hipMemcpyAsync(s.h_out, s.d_out, 256, hipMemcpyDeviceToHost, st));
   s.pending = true;
+  s.probe_runs++;
   return 0;
 }
 

@@ -731,34 +731,44 @@ __device__ __forceinline__ void cache_windows(const RowCtx& c, const MsmPlan& P,
 }
 
 // batch: Horner, x8, identity (requires Z != 0), optional compression, partial point. Four waves
-// form the windows' addition operands, then wave 0 runs the serial chain.
+// form the windows' addition operands, then wave 0 runs the serial chain. The 256-byte result
+// block is assembled in LDS and stored whole to `out` (device) and, when given, to `hout` (the
+// slot's pinned host mirror, written through the device mapping: no copy packet per batch).
 __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
                                                    const uint32_t* __restrict__ win, const int* __restrict__ flags,
-                                                   int want_compress, uint8_t* __restrict__ out) {
+                                                   int want_compress, uint8_t* __restrict__ out,
+                                                   uint8_t* __restrict__ hout) {
   __shared__ uint32_t cached[MSM_MAX_WIN * 64];
   __shared__ uint32_t res[2 * EXT_WORDS];
+  __shared__ uint32_t blk[64];
   if (blockIdx.x != 0) return;
   __builtin_amdgcn_s_setprio(3);   // a serial chain: issue ahead of co-resident bulk waves
   const RowCtx c = row_ctx();
   const uint32_t wave = threadIdx.x >> 6;
+  if (threadIdx.x < 64) blk[threadIdx.x] = 0;
   cache_windows(c, P, 0, slice_W, win, cached, wave, 4);
   __syncthreads();
   if (wave == 0) horner_row(c, P, 0, slice_W, win, cached, res);
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
-  ext_to_canonical_bytes(acc, out + 48);
-  const int bad = flags[FLAG_BAD];
-  reinterpret_cast<int*>(out)[0] = (!bad && ge_is_identity(c8)) ? 0 : 1;
-  reinterpret_cast<int*>(out)[1] = bad;
-  reinterpret_cast<int*>(out)[2] = flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
-  reinterpret_cast<int*>(out)[3] = flags[FLAG_OVF];
-  reinterpret_cast<int*>(out)[44] = flags[FLAG_UNCACHED];   // byte 176, after the partial point
-  if (want_compress) {
-    uint32_t w8[8];
-    ge_compress(c8, w8);
-    for (int j = 0; j < 8; ++j)
-      for (int b = 0; b < 4; ++b) out[16 + 4 * j + b] = (uint8_t)(w8[j] >> (8 * b));
+  if (threadIdx.x == 0) {
+    const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
+    uint8_t* b = reinterpret_cast<uint8_t*>(blk);
+    ext_to_canonical_bytes(acc, b + 48);
+    const int bad = flags[FLAG_BAD];
+    blk[0] = (!bad && ge_is_identity(c8)) ? 0u : 1u;
+    blk[1] = (uint32_t)bad;
+    blk[2] = (uint32_t)flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
+    blk[3] = (uint32_t)flags[FLAG_OVF];
+    blk[44] = (uint32_t)flags[FLAG_UNCACHED];   // byte 176, after the partial point
+    if (want_compress) ge_compress(c8, blk + 4);   // bytes 16..48 (little-endian words)
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    reinterpret_cast<uint32_t*>(out)[threadIdx.x] = blk[threadIdx.x];
+    if (hout) {
+      reinterpret_cast<uint32_t*>(hout)[threadIdx.x] = blk[threadIdx.x];
+      __threadfence_system();   // visible to the host once the stream's completion is observed
+    }
   }
 }
 
@@ -867,12 +877,16 @@ static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t); 
 
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
-                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T) {
+                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip) {
   // one workgroup per bin (sort, then accumulation), then the lane-parallel bin reductions
-  hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end,
-                     buckets);
-  hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
-                     buckets, heads, slice_W, slice_T);
+  // (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
+  if (!(probe_skip & 256))
+    hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end,
+                       buckets);
+  if (!(probe_skip & 32))
+    hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
+                       buckets, heads, slice_W, slice_T);
+  if (probe_skip & 64) return;
   if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
   else if (P.nbin() < REDUCE64_MAX_BINS)
@@ -899,10 +913,10 @@ static bool plan_multi(const MsmPlan& P) {
 }
 
 void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
-                     uint32_t* win, int* flags, int want_compress, uint8_t* out) {
+                     uint32_t* win, int* flags, int want_compress, uint8_t* out, uint8_t* hout) {
   if (plan_multi(P) || P.sum_ranges)
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out, hout);
 }
 
 void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,

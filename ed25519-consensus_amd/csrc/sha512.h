@@ -168,31 +168,43 @@ EDC_HD uint64_t load_be64(const uint8_t* p) {
 EDC_HD uint32_t ld_dword_at(uintptr_t a) { return *reinterpret_cast<const uint32_t*>(a); }
 
 // Big-endian word of the padded message tail starting at message byte j (j may exceed mlen).
-// Full words are assembled from aligned dwords (funnel shifts, v_alignbyte on gfx950); only the
-// last partial word of a message takes the byte path.
+// Every word inside the message, the last partial one included, is assembled the same way from
+// three aligned dwords (funnel shifts, v_alignbyte on gfx950; dword addresses clamped to the one
+// holding the message's last byte, so nothing past the message is read beyond that dword), then
+// the bytes past the end are masked and the 0x80 marker inserted. Lanes hashing messages of
+// different lengths thus take one path per word (a byte-by-byte tail was a divergent branch
+// that every wave of a variable-length batch executed for every word of its last block).
 EDC_HD uint64_t msg_word(const uint8_t* m, uint64_t mlen, uint64_t j) {
-  if (j + 8 <= mlen) {
-    const uintptr_t p = (uintptr_t)(m + j);
-    const uintptr_t a = p & ~(uintptr_t)3;
-    const uint32_t d0 = ld_dword_at(a), d1 = ld_dword_at(a + 4);
-    const uint32_t d2 = ld_dword_at((p + 7) & ~(uintptr_t)3);   // = d1 when p is dword aligned
-#if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t sh = (uint32_t)(p & 3);                       // funnel shifts by bytes, no branch
-    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
-#else
-    const uint32_t sh = (uint32_t)(p & 3) * 8;
-    const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
-    const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
-#endif
-    return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
-  }
   if (j >= mlen) return j == mlen ? (0x80ull << 56) : 0ull;   // padding only: marker or zeros
-  uint64_t w = 0;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    uint64_t i = j + b;
-    uint8_t byte = i < mlen ? m[i] : (i == mlen ? 0x80 : 0);
-    w = (w << 8) | byte;
+  const uintptr_t p = (uintptr_t)(m + j);
+  const uintptr_t last = (uintptr_t)(m + mlen - 1) & ~(uintptr_t)3;
+  const uintptr_t a = p & ~(uintptr_t)3;
+  const uintptr_t a1 = a + 4 < last ? a + 4 : last, a2 = ((p + 7) & ~(uintptr_t)3) < last ? ((p + 7) & ~(uintptr_t)3) : last;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t d0 = ld_dword_at(a), d1 = ld_dword_at(a1), d2 = ld_dword_at(a2);
+#else   // host build (tests/native): the same dwords, without touching bytes past the message
+  const uintptr_t end = (uintptr_t)(m + mlen);
+  auto ld = [end](uintptr_t q) {
+    uint32_t v = 0;
+    for (int b = 0; b < 4; ++b)
+      if (q + b < end) v |= (uint32_t)*reinterpret_cast<const uint8_t*>(q + b) << (8 * b);
+    return v;
+  };
+  const uint32_t d0 = ld(a), d1 = ld(a1), d2 = ld(a2);
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t sh = (uint32_t)(p & 3);                       // funnel shifts by bytes, no branch
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+#else
+  const uint32_t sh = (uint32_t)(p & 3) * 8;
+  const uint32_t lo = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;
+  const uint32_t hi = sh ? (d1 >> sh) | (d2 << (32 - sh)) : d1;
+#endif
+  uint64_t w = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
+  const uint64_t rem = mlen - j;                               // >= 1
+  if (rem < 8) {                                               // keep rem bytes, then the marker
+    const uint32_t kb = 8 * (uint32_t)rem;
+    w = (w & (~0ull << (64 - kb))) | (0x80ull << (56 - kb));
   }
   return w;
 }

@@ -80,7 +80,7 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
 /*
  * Asynchronous form of edc_batch_verify_device for streams of batches (a consensus node
  * verifying block after block): edc_batch_submit_device enqueues the whole pipeline on one of the
- * context's in-flight slots (8) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
+ * context's in-flight slots (16) and returns a ticket >= 0 (or <0); edc_batch_wait blocks for that
  * ticket and returns its verdict (EDC_OK / EDC_INVALID_SIGNATURE, <0 on runtime failure), with
  * optional check8 (needs want_check8), partial point and bad flag. Tickets must be waited in
  * submission order before their slot is reused; inputs must stay valid until the wait.
@@ -292,9 +292,9 @@ int edc_debug_set_scatter_stage(uint32_t max_entries);
 int edc_set_fallback_shape(edc_ctx* ctx, int ranges, int bits);
 
 /*
- * Number of in-flight slots (1..8, default 8) this context's submissions rotate over; each slot
+ * Number of in-flight slots (1..16, default 16) this context's submissions rotate over; each slot
  * holds its own workspace and hardware queue. Contexts that share one GPU (edc_create_multi with
- * a repeated device) get 8 / (contexts on that GPU). Refused while batches are in flight.
+ * a repeated device) get 16 / (contexts on that GPU). Refused while batches are in flight.
  */
 int edc_set_slots(edc_ctx* ctx, int k);
 
@@ -343,7 +343,7 @@ int edc_multi_batch_verify(edc_multi* m, size_t n, const uint8_t* vk, const uint
  * waiting. Each shard's 128-byte partial point (with its bad flag) is copied device to device to
  * the first device (peer copy over xGMI), where a combine on its own stream sums the partials
  * (x8, identity) as soon as the last shard lands. edc_multi_wait blocks for the ticket and
- * returns EDC_OK / EDC_INVALID_SIGNATURE / <0 with optional check8 (needs want_check8). Up to 8
+ * returns EDC_OK / EDC_INVALID_SIGNATURE / <0 with optional check8 (needs want_check8). Up to 16
  * batches in flight; tickets are waited in submission order; host buffers are borrowed until the
  * wait. edc_multi_submit_device takes per-device slices already resident in each device's HBM:
  * n[g] items at d_vk[g], d_sig[g], d_msg[g], d_msg_off[g] form shard g, with global queue indices

@@ -126,7 +126,7 @@ def test_multi_submit_device_config3(multi, engine):
     starts = off[:-1][idx]
     msg2 = torch.cat([msg[(starts[:, None] + cols)[cols < lens[:, None]]], torch.zeros(1, dtype=torch.uint8, device=dev)])
     n2 = len(idx)
-    # two batches in flight per context at most (contexts sharing one GPU split its 8 slots)
+    # two batches in flight per context at most (contexts sharing one GPU split its slots)
     sh2 = shards(vk2, sig2, msg2, off2, n2)
     t_ok = [multi.batch_submit_device(sh2, zs, want_check8=True)]
     code, _ = multi.batch_wait(t_bad, want_check8=True)
