@@ -583,7 +583,7 @@ __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_
 // About 4x the instructions of k_msm_reduce, so large batches keep the lane-parallel form.
 constexpr uint32_t REDUCE_QUAD_MAX_BINS = 128;
 #ifndef EDC_REDUCE64_MAX_BINS
-#define EDC_REDUCE64_MAX_BINS 512
+#define EDC_REDUCE64_MAX_BINS 256
 #endif
 constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per bin below this many bins
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
@@ -608,15 +608,15 @@ __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restr
 }
 
 // Win(range g, window w) = sum_s W_s + 256 * sum_s s T_s over the window's slices, for windows
-// with more than one slice (single-slice windows are read straight from their bin). One
-// workgroup per (range, window).
-__global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* __restrict__ slice_W,
-                                                    const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t g = blockIdx.x / P.nwin, w = blockIdx.x % P.nwin;
+// with more than one slice (single-slice windows are read straight from their bin): one
+// 256-lane workgroup, `smem` = kReduceLds bytes of LDS.
+__device__ __forceinline__ bool window_needs_combine(const MsmPlan& P, uint32_t w) {
+  return P.nslice[w] * P.nsub[w] > 1 || P.sum_ranges;
+}
+__device__ __forceinline__ void window_combine(const MsmPlan& P, uint32_t g, uint32_t w, const uint32_t* __restrict__ slice_W,
+                                               const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win,
+                                               uint32_t* smem) {
   const uint32_t ns = P.nslice[w], nsub = P.nsub[w];
-  if (ns * nsub <= 1 && !P.sum_ranges) return;
-  __builtin_amdgcn_s_setprio(3);   // latency-bound tail: issue ahead of co-resident bulk waves
   const int t = threadIdx.x;
   const uint32_t b0 = g * P.bins_per_range + P.bin0[w];
   // slice t's sums: its sub-bins, and the parts of one batch (sum_ranges), are added first
@@ -647,6 +647,16 @@ __global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* _
     for (int k = 0; k < SLICE_BITS; ++k) x = row_dbl(c, x);
     row_st_ext(c, win + ((size_t)g * MSM_MAX_WIN + w) * EXT_WORDS, row_add(c, x, bq));
   }
+}
+
+// One workgroup per (range, window) (grouped fallback ranges).
+__global__ void __launch_bounds__(256) k_msm_window(MsmPlan P, const uint32_t* __restrict__ slice_W,
+                                                    const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t g = blockIdx.x / P.nwin, w = blockIdx.x % P.nwin;
+  if (!window_needs_combine(P, w)) return;
+  __builtin_amdgcn_s_setprio(3);   // latency-bound tail: issue ahead of co-resident bulk waves
+  window_combine(P, g, w, slice_W, slice_T, win, smem);
 }
 
 __device__ __forceinline__ void fe_to_bytes32(const fe& a, uint8_t* out) {
@@ -710,10 +720,12 @@ __device__ __forceinline__ const uint32_t* window_ptr(const MsmPlan& P, uint32_t
 // form of every window but the top one (row_cached, one word per lane, 64 words per window);
 // returns Win and [8]Win in `res` (two extended points, X | Y | Z | T).
 __device__ __forceinline__ void horner_row(const RowCtx& c, const MsmPlan& P, uint32_t g, const uint32_t* slice_W,
-                                           const uint32_t* win, const uint32_t* cached, uint32_t* res) {
+                                           const uint32_t* win, const uint32_t* cached, uint32_t* res,
+                                           const uint32_t* from = nullptr, uint32_t from_w = 0) {
+  // from: the Horner value after windows from_w..nwin-1 (k_msm_window2), else start at the top
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t acc = row_ld_ext(c, window_ptr(P, g, P.nwin - 1, slice_W, win));
-  for (int w = (int)P.nwin - 2; w >= 0; --w) {
+  uint32_t acc = row_ld_ext(c, from ? from : window_ptr(P, g, P.nwin - 1, slice_W, win));
+  for (int w = (from ? (int)from_w : (int)P.nwin - 1) - 1; w >= 0; --w) {
     const uint32_t bq = cached[w * 64 + lane];
     for (uint32_t k = 0; k < P.bits[w]; ++k) acc = row_dbl(c, acc);
     acc = row_add(c, acc, bq);
@@ -725,9 +737,11 @@ __device__ __forceinline__ void horner_row(const RowCtx& c, const MsmPlan& P, ui
 
 // second-operand forms of range g's windows 0..nwin-2 into cached[] by the workgroup's `nwave` waves
 __device__ __forceinline__ void cache_windows(const RowCtx& c, const MsmPlan& P, uint32_t g, const uint32_t* slice_W,
-                                              const uint32_t* win, uint32_t* cached, uint32_t wave, uint32_t nwave) {
+                                              const uint32_t* win, uint32_t* cached, uint32_t wave, uint32_t nwave,
+                                              uint32_t upto = MSM_MAX_WIN) {
   const uint32_t d2 = row_d2(c), lane = threadIdx.x & 63;
-  for (uint32_t w = wave; w + 1 < P.nwin; w += nwave) cached[w * 64 + lane] = row_cached(c, window_ptr(P, g, w, slice_W, win), d2);
+  for (uint32_t w = wave; w + 1 < P.nwin && w < upto; w += nwave)
+    cached[w * 64 + lane] = row_cached(c, window_ptr(P, g, w, slice_W, win), d2);
 }
 
 // batch: Horner, x8, identity (requires Z != 0), optional compression, partial point. Four waves
@@ -737,7 +751,8 @@ __device__ __forceinline__ void cache_windows(const RowCtx& c, const MsmPlan& P,
 __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
                                                    const uint32_t* __restrict__ win, const int* __restrict__ flags,
                                                    int want_compress, uint8_t* __restrict__ out,
-                                                   uint8_t* __restrict__ hout) {
+                                                   uint8_t* __restrict__ hout, const uint32_t* __restrict__ from,
+                                                   uint32_t from_w) {
   __shared__ uint32_t cached[MSM_MAX_WIN * 64];
   __shared__ uint32_t res[2 * EXT_WORDS];
   __shared__ uint32_t blk[64];
@@ -746,9 +761,9 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
   const RowCtx c = row_ctx();
   const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x < 64) blk[threadIdx.x] = 0;
-  cache_windows(c, P, 0, slice_W, win, cached, wave, 4);
+  cache_windows(c, P, 0, slice_W, win, cached, wave, 4, from ? from_w : MSM_MAX_WIN);
   __syncthreads();
-  if (wave == 0) horner_row(c, P, 0, slice_W, win, cached, res);
+  if (wave == 0) horner_row(c, P, 0, slice_W, win, cached, res, from, from_w);
   __syncthreads();
   if (threadIdx.x == 0) {
     const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
@@ -770,6 +785,44 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
       __threadfence_system();   // visible to the host once the stream's completion is observed
     }
   }
+}
+
+// Batch tail with the top-run Horner overlapped (plans whose top windows need no combine: for
+// vote batches the 16 single-bin 8-bit windows of bits 128..252, ~125 doublings). k_msm_window2
+// runs nwin + 1 workgroups: 0..nwin-1 combine the windows that have several slices, the extra one
+// runs the Horner over windows r..nwin-1 into `hbuf` at the same time; k_msm_final then continues
+// the Horner from hbuf over windows r-1..0. Serial depth: max(window combine, top-run Horner) +
+// the rest of the Horner, instead of their sum. (A single launch with an arrival counter needs an
+// L2 writeback per workgroup for the hand-off and measured slower.)
+__host__ __device__ __forceinline__ uint32_t top_run_start(const MsmPlan& P) {
+  uint32_t r = P.nwin;
+  while (r > 0 && !(P.nslice[r - 1] * P.nsub[r - 1] > 1 || P.sum_ranges)) --r;
+  return r;
+}
+__global__ void __launch_bounds__(256) k_msm_window2(MsmPlan P, const uint32_t* __restrict__ slice_W,
+                                                     const uint32_t* __restrict__ slice_T, uint32_t* __restrict__ win,
+                                                     uint32_t* __restrict__ hbuf) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __builtin_amdgcn_s_setprio(3);
+  if (blockIdx.x < P.nwin) {
+    if (window_needs_combine(P, blockIdx.x)) window_combine(P, 0, blockIdx.x, slice_W, slice_T, win, smem);
+    return;
+  }
+  const uint32_t r = top_run_start(P);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t* cached = smem;                              // windows r..nwin-2, 64 words each
+  const RowCtx c = row_ctx();
+  const uint32_t d2 = row_d2(c);
+  for (uint32_t w = r + wave; w + 1 < P.nwin; w += 4) cached[w * 64 + lane] = row_cached(c, window_ptr(P, 0, w, slice_W, win), d2);
+  __syncthreads();
+  if (wave != 0) return;
+  uint32_t acc = row_ld_ext(c, window_ptr(P, 0, P.nwin - 1, slice_W, win));
+  for (int w = (int)P.nwin - 2; w >= (int)r; --w) {
+    const uint32_t bq = cached[w * 64 + lane];
+    for (uint32_t k = 0; k < P.bits[w]; ++k) acc = row_dbl(c, acc);
+    acc = row_add(c, acc, bq);
+  }
+  row_st_ext(c, hbuf, acc);
 }
 
 // ranges: rverdict[g] = 0 iff [8] * (range g's check point) is the identity; one wave per range
@@ -914,9 +967,19 @@ static bool plan_multi(const MsmPlan& P) {
 
 void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out, uint8_t* hout) {
+  const uint32_t r = top_run_start(P);
+  if (plan_multi(P) && r < P.nwin && r > 0 && P.nwin < MSM_MAX_WIN) {
+    // window combines beside the top-run Horner; hbuf = the unused last window record of range 0
+    uint32_t* hbuf = win + (size_t)(MSM_MAX_WIN - 1) * EXT_WORDS;
+    hipLaunchKernelGGL(k_msm_window2, dim3(P.nwin + 1), dim3(256), kReduceLds, st, P, slice_W, slice_T, win, hbuf);
+    hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out, hout,
+                       (const uint32_t*)hbuf, r);
+    return;
+  }
   if (plan_multi(P) || P.sum_ranges)
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
-  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out, hout);
+  hipLaunchKernelGGL(k_msm_final, dim3(1), dim3(256), 0, st, P, slice_W, win, flags, want_compress, out, hout,
+                     (const uint32_t*)nullptr, 0u);
 }
 
 void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=r03p
+t=${TAG:-r03p}
 D=ed25519-consensus_amd/csrc
 timeout -k 10 300 python -u -m pytest tests/test_gpu_multiblock.py tests/test_gpu_parity.py tests/test_gpu_config4.py tests/test_gpu_edges.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${t}_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -2 gpurun_out/${t}_tests.log; [ $rc -eq 0 ] || exit $rc
@@ -12,5 +12,5 @@ ab() {
   echo "$3 $2 $(tail -1 gpurun_out/${t}.log | grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"challenge_sha512": [0-9.]*' | tr '\n' ' ')" | tee -a gpurun_out/${t}_all.log
 }
 for rep in 1 2; do
-  for lib in hw sha; do ab "--config c5 --steps 20" $lib c5; ab "--config c3 --steps 40" $lib c3; ab "--config c2 --inflight 16 --steps 40" $lib c2; done
+  for lib in sha sort; do ab "--config c5 --steps 20" $lib c5; ab "--config c3 --steps 40" $lib c3; ab "--config c2 --inflight 16 --steps 40" $lib c2; done
 done
