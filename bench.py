@@ -187,7 +187,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
-    ap.add_argument("--inflight", type=int, default=6, help="batches in flight per GPU (submit/wait pipelining, <= the build's slot count, 8)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight per GPU (submit/wait pipelining, <= the context's 16 slots); "
+                         "0 = 6 from 2^19 signatures per GPU up, 16 below (small shards need more overlap)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
@@ -232,6 +234,14 @@ def main():
 
     n = args.n // world if args.scaling == "strong" else args.n
     base = rank * n
+    # ranks sharing one GPU (the gloo rehearsal) split its in-flight slots: past ~16 user queues
+    # per GPU the hardware scheduler time-slices them ("One hardware queue per slot")
+    sharing = max(1, -(-world // max(1, torch.cuda.device_count()))) if backend == "gloo" else 1
+    slots = max(1, 16 // sharing)
+    eng._check(eng.lib.edc_set_slots(eng.ctx, slots))
+    if args.inflight <= 0:
+        args.inflight = 6 if n >= (1 << 19) else 16
+    args.inflight = min(args.inflight, slots)
     t_gen = time.perf_counter()
     vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
     torch.cuda.synchronize()
