@@ -407,7 +407,10 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
   }
 }
 
-__global__ void __launch_bounds__(256, 4) k_msm_accum_dma(const uint32_t* __restrict__ counts,
+#ifndef EDC_ACC_OCC
+#define EDC_ACC_OCC 4
+#endif
+__global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32_t* __restrict__ counts,
                                                                    const uint32_t* __restrict__ offsets,
                                                                    const uint32_t* __restrict__ sorted,
                                                                    const uint32_t* __restrict__ bucket_end,
