@@ -47,6 +47,16 @@ EDC_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
 #endif
 }
 
+// One product of a carried column: the chain alternates the asm form (even steps) with LLVM's own
+// mul + add (odd steps, which it forms into v_mad_u64_u32 with the running sum as addend). A single
+// plain step between two asm statements cannot be reassociated, and it separates the asm
+// statements: two back-to-back dependent asm statements cost a hazard wait state (s_nop) on
+// gfx950, since the compiler cannot see what the first one was.
+EDC_HD void mad_step(uint64_t& acc, int j, uint32_t x, uint32_t y) {
+  if (j & 1) acc += mul64(x, y);
+  else acc = mad64(x, y, acc);
+}
+
 EDC_HD fe fe_zero() { fe r; for (int i = 0; i < 9; ++i) r.v[i] = 0; return r; }
 EDC_HD fe fe_one() { fe r = fe_zero(); r.v[0] = 1; return r; }
 
@@ -129,10 +139,11 @@ EDC_HD fe fe_mul(const fe& a, const fe& b) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    if (k < 8) acc = mad64((uint32_t)h[k], 1216u, acc);
-    if (k >= 1) acc = mad64((uint32_t)(h[k - 1] >> 32), 9728u, acc);
+    int j = 0;
+    if (k < 8) mad_step(acc, j++, (uint32_t)h[k], 1216u);
+    if (k >= 1) mad_step(acc, j++, (uint32_t)(h[k - 1] >> 32), 9728u);
 #pragma unroll
-    for (int i = 0; i <= k; ++i) acc = mad64(a.v[i], b.v[k - i], acc);
+    for (int i = 0; i <= k; ++i) mad_step(acc, j++, a.v[i], b.v[k - i]);
     r.v[k] = (uint32_t)acc & M29;
     acc >>= 29;
   }
@@ -156,11 +167,12 @@ EDC_HD fe fe_sqr(const fe& a) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    if (k < 8) acc = mad64((uint32_t)h[k], 1216u, acc);
-    if (k >= 1) acc = mad64((uint32_t)(h[k - 1] >> 32), 9728u, acc);
+    int j = 0;
+    if (k < 8) mad_step(acc, j++, (uint32_t)h[k], 1216u);
+    if (k >= 1) mad_step(acc, j++, (uint32_t)(h[k - 1] >> 32), 9728u);
 #pragma unroll
-    for (int i = 0; 2 * i < k; ++i) acc = mad64(a.v[i], d[k - i], acc);
-    if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
+    for (int i = 0; 2 * i < k; ++i) mad_step(acc, j++, a.v[i], d[k - i]);
+    if ((k & 1) == 0) mad_step(acc, j++, a.v[k / 2], a.v[k / 2]);
     r.v[k] = (uint32_t)acc & M29;
     acc >>= 29;
   }
