@@ -589,6 +589,10 @@ constexpr uint32_t REDUCE_QUAD_MAX_BINS = 128;
 #define EDC_REDUCE64_MAX_BINS 256
 #endif
 constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per bin below this many bins
+#ifndef EDC_REDUCE_WIDE_LANES
+#define EDC_REDUCE_WIDE_LANES 32
+#endif
+constexpr int REDUCE_WIDE_LANES = EDC_REDUCE_WIDE_LANES;          // lanes per bin from that many bins up
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ buckets,
                                                          uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
@@ -949,8 +953,8 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
                        slice_T);
   else
-    hipLaunchKernelGGL(k_msm_reduce<32>, dim3(cdiv(P.nbin(), 8)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
-                       slice_T);
+    hipLaunchKernelGGL(k_msm_reduce<REDUCE_WIDE_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_WIDE_LANES)), dim3(256), 0, st,
+                       P.nbin(), counts, buckets, slice_W, slice_T);
 }
 
 #ifdef EDC_STAMPS

@@ -16,7 +16,10 @@ namespace edc {
 
 constexpr int SHA_CLASSES = 16;   // block counts 1..14, 15+, and out-of-range lanes
 constexpr int SHA_THREADS = 256;  // items regrouped per workgroup
-__global__ void __launch_bounds__(SHA_THREADS, 4) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
+#ifndef EDC_SHA_OCC
+#define EDC_SHA_OCC 4
+#endif
+__global__ void __launch_bounds__(SHA_THREADS, EDC_SHA_OCC) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
                                                    const uint8_t* __restrict__ sig,
                                                    const uint8_t* __restrict__ msg,
                                                    const uint64_t* __restrict__ off,

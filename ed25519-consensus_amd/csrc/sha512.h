@@ -215,6 +215,9 @@ EDC_HD void sha512_src_state(const sha_src& s, uint64_t h[8]) {
   const uint64_t hlen = s.head1 ? 64 : 32;
   const uint64_t total = hlen + s.mlen;
   const uint64_t nblocks = (total + 17 + 127) / 128;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t pf0 = 0, pf1 = 0;
+#endif
 #pragma unroll 1
   for (uint64_t blk = 0; blk < nblocks; ++blk) {
     uint64_t w[16];
@@ -229,7 +232,23 @@ EDC_HD void sha512_src_state(const sha_src& s, uint64_t h[8]) {
       w[14] = 0;                 // bit-length high word (messages < 2^61 bytes)
       w[15] = total << 3;
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    // touch the next block's message lines (both 64-byte halves) so that they are on their way
+    // to the caches while this block compresses; the loaded values are never used
+    if (blk + 1 < nblocks && s.mlen) {
+      const uint64_t j0 = (blk + 1) * 128 - hlen;
+      const uintptr_t lo = (uintptr_t)s.msg, hi = ((uintptr_t)(s.msg + s.mlen - 1)) & ~(uintptr_t)3;
+      uintptr_t q0 = (lo + j0) & ~(uintptr_t)3, q1 = (lo + j0 + 124) & ~(uintptr_t)3;
+      q0 = q0 < hi ? q0 : hi;
+      q1 = q1 < hi ? q1 : hi;
+      pf0 = *reinterpret_cast<const uint32_t*>(q0);
+      pf1 = *reinterpret_cast<const uint32_t*>(q1);
+    }
+#endif
     sha512_compress(h, w);
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(pf0), "v"(pf1));   // consumed after the compression: the loads stay in flight over it
+#endif
   }
 }
 
