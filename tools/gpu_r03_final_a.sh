@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=r03f
+t=${TAG:-r03f}
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${t}_gpu_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -2 gpurun_out/${t}_gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${t}_smoke.log 2>&1 || { tail -5 gpurun_out/${t}_smoke.log; exit 1; }

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=r03f
+t=${TAG:-r03f}
 run() {  # name args...
   local name=$1; shift
   timeout -k 10 300 python3 bench.py "$@" --no-cpu-baseline > gpurun_out/${t}_bench_$name.log 2>&1 || { echo ${name}_fail; tail -5 gpurun_out/${t}_bench_$name.log; exit 1; }
