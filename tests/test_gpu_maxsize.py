@@ -87,3 +87,54 @@ def test_key_indexed_stream_equals_device_path_2_20(engine):
             assert (c8.raw == bytes([1]) + bytes(31)) != corrupt
     finally:
         engine.keycache_clear()
+
+
+def test_strong_scaling_shard_2_17(engine):
+    """The 2^17 shard of a 2^20 vote batch split over 8 GPUs (auto plan: 15-bit windows, the
+    overlapped tail once the context has seen the key ratio): a valid shard is Ok with the
+    identity twice (grouped, then with the few-keys hint); one corrupted signature makes it fail
+    with a non-identity [8]*check that 4 sub-shards at global z offsets reproduce through
+    edc_batch_partial_device + edc_combine_partials, and the grouped fallback finds exactly that
+    item."""
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, ROOT)
+    import bench
+    dev = torch.device("cuda:0")
+    n, keys = 1 << 17, 150
+    pkg = sys.modules["ed25519_consensus_amd"]
+    vk, sig, msg, off = bench.make_workload(pkg, engine, torch, dev, n, keys, 120, 3 * n)
+    torch.cuda.synchronize()
+    lib = engine.lib
+    zseed = bytes([0x2B]) * 32
+    c8 = ctypes.create_string_buffer(32)
+
+    def verify():
+        return lib.edc_batch_verify_device(engine.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                           off.data_ptr(), zseed, 3 * n, None, c8)
+
+    ident = bytes([1]) + bytes(31)
+    assert verify() == 0 and c8.raw == ident
+    assert verify() == 0 and c8.raw == ident
+    bad = 99_999
+    sig[64 * bad + 7] ^= 0x40                                      # R changed
+    torch.cuda.synchronize()
+    assert verify() == 1 and c8.raw != ident
+    whole = c8.raw
+    parts, bad_any = [], 0
+    for g in range(4):
+        lo, hi = n * g // 4, n * (g + 1) // 4
+        o = (off[lo:hi + 1] - off[lo]).contiguous()
+        part = ctypes.create_string_buffer(128)
+        flag = ctypes.c_int(0)
+        assert lib.edc_batch_partial_device(engine.ctx, hi - lo, vk.data_ptr() + 32 * lo, sig.data_ptr() + 64 * lo,
+                                            msg.data_ptr() + int(off[lo].item()), o.data_ptr(), zseed, 3 * n + lo,
+                                            None, part, ctypes.byref(flag)) == 0
+        parts.append(part.raw)
+        bad_any |= flag.value
+    assert engine.combine_partials(parts, bad_any) == (1, whole)
+    verdicts = ctypes.create_string_buffer(n)
+    # the fallback draws z from the same seed at indices 0.. (its own batch), as the reference's
+    # verify_single loop needs no z at all: only the verdicts are compared
+    assert lib.edc_find_invalid_device(engine.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
+                                       zseed, 1 << 14, verdicts) == 1
+    assert verdicts.raw[bad] != 0 and verdicts.raw.count(0) == n - 1

@@ -3,7 +3,7 @@ the C oracle (dalek algorithm: Straus below 190 terms, Pippenger w = 6/7/8 above
 compressed [8]*check, bit-exact, for valid batches and for batches whose check point is NOT the
 identity (one bad item).
 
-Plans covered: window widths 9..16 and the size-chosen default, one batch split into 1..16
+Plans covered: window widths 9..16 (14 and 15 are the auto widths from 2^17) and the size-chosen default, one batch split into 1..16
 parts (summed per window); 8-bit high windows for the B / key
 coefficients (chosen when the previous grouped batch on the context had few distinct keys) and
 full-width windows otherwise; grouped keys, one key term per signature, and the on-device overflow
@@ -40,7 +40,7 @@ def _batch(engine, n, m, bad, msg_len=120, seed=0):
 
 @pytest.mark.parametrize("n,m,bad", [(4096, 256, None), (4096, 256, 77), (4096, 257, 5), (8192, 5, 8000),
                                      (8192, 1, None), (8192, 150, 3), (6000, 6000, 17)])
-@pytest.mark.parametrize("bits,parts", [(0, 0), (9, 1), (12, 3), (13, 0), (16, 1), (16, 2), (11, 16)])
+@pytest.mark.parametrize("bits,parts", [(0, 0), (9, 1), (12, 3), (13, 0), (14, 1), (15, 1), (16, 1), (16, 2), (11, 16)])
 def test_plans_match_oracle(engine, oracle_c, n, m, bad, bits, parts):
     vks, sigs, msgs, zseed = _batch(engine, n, m, bad)
     exp_code, exp_c8 = oracle_c.batch_verify(list(zip(vks, sigs, msgs)), zseed)
