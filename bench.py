@@ -238,7 +238,8 @@ def main():
     # per GPU the hardware scheduler time-slices them ("One hardware queue per slot")
     sharing = max(1, -(-world // max(1, torch.cuda.device_count()))) if backend == "gloo" else 1
     slots = max(1, 16 // sharing)
-    eng._check(eng.lib.edc_set_slots(eng.ctx, slots))
+    if sharing > 1:
+        eng._check(eng.lib.edc_set_slots(eng.ctx, slots))
     if args.inflight <= 0:
         args.inflight = 6 if n >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)

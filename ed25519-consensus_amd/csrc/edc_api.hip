@@ -40,6 +40,9 @@ constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
 #define EDC_PROBE_SKIP 0
 #endif
 #define EDC_RUN(bit) ((EDC_PROBE_SKIP & (bit)) == 0 || s.probe_runs == 0)
+#ifndef EDC_DUAL_STREAM
+#define EDC_DUAL_STREAM 0
+#endif
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
 }  // namespace
@@ -68,6 +71,10 @@ struct Slot {
   uint8_t* d_out = nullptr;     // 256-byte result block
   uint8_t* h_out = nullptr;     // pinned mirror
   hipEvent_t ev[PH_N + 1] = {};
+  // EDC_DUAL_STREAM builds: the decode runs on a second stream beside SHA-512 / coefficients /
+  // binning (joined before the accumulation)
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_keys = nullptr, ev_dec = nullptr;
   // host-buffer submissions (edc_batch_submit): this slot's own device copy of the inputs
   uint8_t *in_vk = nullptr, *in_sig = nullptr, *in_msg = nullptr;
   uint64_t* in_off = nullptr;
@@ -203,6 +210,15 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   CK(dalloc(&s.d_out, 256));
   CK(hipHostMalloc((void**)&s.h_out, 256));
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
+#if EDC_DUAL_STREAM
+  // 1: every slot; 2: slot 0 only (the synchronous calls' slot), so the pipelined slots keep one
+  // hardware queue each (past ~16 user queues per GPU the scheduler time-slices them)
+  if (EDC_DUAL_STREAM == 1 || &s == &ctx->slot[0]) {
+    CK(create_slot_stream(ctx->device, &s.st2));
+    CK(hipEventCreateWithFlags(&s.ev_keys, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&s.ev_dec, hipEventDisableTiming));
+  }
+#endif
   return 0;
 }
 
@@ -226,7 +242,7 @@ static int ensure_slot(edc_ctx* ctx, Slot& s, size_t n) {
   CK(dalloc(&s.key_acc, cap * KEY_ACC_LIMBS));
   CK(dalloc(&s.u_acc, (cap / COEF_CHUNK + 2) * KEY_ACC_LIMBS));   // one sum per fallback range
   CK(dalloc(&s.coef_part, coef_part_words(cap)));
-  CK(dalloc(&s.itembad, cap));
+  CK(dalloc(&s.itembad, 2 * cap));   // [0, cap): s bits (k_coef), [cap, 2 cap): R bits (k_decompress)
   CK(dalloc(&s.keybad, cap));
   launch_init_basepoint(s.st, s.pts);
   CK(hipGetLastError());
@@ -580,6 +596,18 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
     launch_keys(st, N, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
                 s.key_index, s.key_acc, s.flags);
   }
+  // dual-stream builds (untimed batches): the decode only needs the key grouping, so it runs on
+  // the slot's second stream beside SHA-512 / coefficients / binning; its per-item R bits go to
+  // their own array (itembad + cap_n), so no byte is written by both streams
+  const bool dual = EDC_DUAL_STREAM && s.st2 && !s.timed;
+  if (dual) {
+    CK(hipEventRecord(s.ev_keys, st));
+    CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
+    if (EDC_RUN(16))
+      launch_decompress(s.st2, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags,
+                        ctx->kc(), split);
+    CK(hipEventRecord(s.ev_dec, s.st2));
+  }
   mark(PH_CHALLENGE);
   if (EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
@@ -592,7 +620,10 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
-  if (EDC_RUN(16)) launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad, s.keybad, s.flags, ctx->kc(), split);
+  if (dual) CK(hipStreamWaitEvent(st, s.ev_dec, 0));
+  else if (EDC_RUN(16))
+    launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
+                      split);
   CK(hipGetLastError());
   return 0;
 }
@@ -732,6 +763,9 @@ void edc_destroy(edc_ctx* ctx) {
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
     if (s.st) (void)hipStreamDestroy(s.st);
+    if (s.st2) (void)hipStreamDestroy(s.st2);
+    if (s.ev_keys) (void)hipEventDestroy(s.ev_keys);
+    if (s.ev_dec) (void)hipEventDestroy(s.ev_dec);
   }
   {
     Slot& s = ctx->comb;
@@ -1049,7 +1083,8 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
                     s.slice_T);
   launch_msm_range_tail(st, P, s.slice_W, s.slice_T, s.win, ctx->fb_rv);
   CK(hipMemsetAsync(ctx->fb_rv + G, 0, G, st));
-  launch_range_prebad(st, (uint32_t)n, (uint32_t)rsize, s.itembad, s.keybad, s.key_index, per_sig, ctx->fb_rv + G);
+  launch_range_prebad(st, (uint32_t)n, (uint32_t)rsize, s.itembad, s.itembad + s.cap_n, s.keybad, s.key_index, per_sig,
+                      ctx->fb_rv + G);
   CK(hipGetLastError());
   std::vector<uint8_t> rv(2 * (size_t)G);
   CK(hipMemcpyAsync(rv.data(), ctx->fb_rv, 2 * (size_t)G, hipMemcpyDeviceToHost, st));

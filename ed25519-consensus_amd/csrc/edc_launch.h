@@ -27,7 +27,8 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
                        const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],
                        uint64_t zbase, const uint32_t* key_index, uint32_t* scal, unsigned long long* key_acc,
                        unsigned long long* u_acc, int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal);
-void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* keybad,
+void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* itembad_r,
+                         const uint8_t* keybad,
                          const uint32_t* key_index, bool per_sig, uint8_t* rbad);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const uint8_t* vk, const uint8_t* sig,

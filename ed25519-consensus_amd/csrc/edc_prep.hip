@@ -88,7 +88,7 @@ __device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
 __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep, int per_sig_host,
-                                                       uint32_t* __restrict__ pts, uint8_t* __restrict__ itembad,
+                                                       uint32_t* __restrict__ pts, uint8_t* __restrict__ itembad_r,
                                                        uint8_t* __restrict__ keybad, int* __restrict__ flags,
                                                        KeyCacheView kcache, int split) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -98,10 +98,8 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
     st_niels(pts, 1 + i, ge_to_niels_affine(P));
-    if (!ok) {
-      itembad[i] |= ITEM_BAD_R;
-      atomicOr(&flags[FLAG_BAD], 1);
-    }
+    itembad_r[i] = ok ? 0 : ITEM_BAD_R;   // its own array: k_coef writes the s bits concurrently
+    if (!ok) atomicOr(&flags[FLAG_BAD], 1);
     return;
   }
   const uint32_t kbase = (n + 63u) & ~63u;   // key lanes start on a wave boundary (no R/key divergence)
@@ -552,12 +550,13 @@ __global__ void __launch_bounds__(256) k_range_terms(uint32_t n, uint32_t nrange
 // Range mode: rbad[g] = 1 iff range g holds an item whose R or s failed, or whose key failed to
 // decode (such ranges are verified item by item whatever their partial point).
 __global__ void __launch_bounds__(256) k_range_prebad(uint32_t n, uint32_t rsize, const uint8_t* __restrict__ itembad,
+                                                      const uint8_t* __restrict__ itembad_r,
                                                       const uint8_t* __restrict__ keybad,
                                                       const uint32_t* __restrict__ key_index, int per_sig,
                                                       uint8_t* __restrict__ rbad) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (itembad[i] || keybad[per_sig ? i : key_index[i]]) rbad[i / rsize] = 1;
+  if (itembad[i] || itembad_r[i] || keybad[per_sig ? i : key_index[i]]) rbad[i / rsize] = 1;
 }
 
 __global__ void k_init_basepoint(uint32_t* pts) {
@@ -661,11 +660,12 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }
-void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* keybad,
+void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* itembad_r,
+                         const uint8_t* keybad,
                          const uint32_t* key_index, bool per_sig, uint8_t* rbad) {
   if (n)
-    hipLaunchKernelGGL(k_range_prebad, dim3(cdiv(n, 256)), dim3(256), 0, st, n, rsize, itembad, keybad, key_index,
-                       per_sig ? 1 : 0, rbad);
+    hipLaunchKernelGGL(k_range_prebad, dim3(cdiv(n, 256)), dim3(256), 0, st, n, rsize, itembad, itembad_r, keybad,
+                       key_index, per_sig ? 1 : 0, rbad);
 }
 // Key-indexed host submissions (edc_batch_submit_indexed): item i's raw key bytes from the key
 // cache, vk_out[i] = keys[reg[key_idx[i]]] (indices were range-checked on the host), so the

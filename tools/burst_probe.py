@@ -20,13 +20,14 @@ def main():
     ap.add_argument("--keys", type=int, default=150)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ks", default="1,2,3,4,5,6,8")
+    ap.add_argument("--lib", default=None, help="A/B build of libedc.so (measurement only)")
     a = ap.parse_args()
     import torch
     import bench
     dev = torch.device("cuda:0")
     torch.zeros(1, device=dev)
     pkg = bench.load_pkg()
-    eng = pkg.Engine(0)
+    eng = pkg.Engine(0, lib_path=a.lib)
     lib = eng.lib
     zseed = bytes([0x33]) * 32
     n = a.n
