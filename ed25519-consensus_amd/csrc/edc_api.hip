@@ -41,7 +41,7 @@ constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
 #endif
 #define EDC_RUN(bit) ((EDC_PROBE_SKIP & (bit)) == 0 || s.probe_runs == 0)
 #ifndef EDC_DUAL_STREAM
-#define EDC_DUAL_STREAM 0
+#define EDC_DUAL_STREAM 2   // slot 0 (synchronous calls) decodes on a second stream; see init_slot
 #endif
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
 
