@@ -238,11 +238,13 @@ def main():
     # per GPU the hardware scheduler time-slices them ("One hardware queue per slot")
     sharing = max(1, -(-world // max(1, torch.cuda.device_count()))) if backend == "gloo" else 1
     slots = max(1, 16 // sharing)
-    if sharing > 1:
-        eng._check(eng.lib.edc_set_slots(eng.ctx, slots))
     if args.inflight <= 0:
         args.inflight = 6 if n >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)
+    # the context rotates over exactly `inflight` slots, so only that many slot streams (hardware
+    # queues) exist beside RCCL's own in a multi-rank run; a build with fewer slots keeps its count
+    if eng.lib.edc_set_slots(eng.ctx, args.inflight) < 0 and sharing > 1:
+        raise RuntimeError("cannot split the GPU's slots between the ranks sharing it")
     t_gen = time.perf_counter()
     vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
     torch.cuda.synchronize()
