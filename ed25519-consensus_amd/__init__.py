@@ -46,6 +46,9 @@ ABI_SYMBOLS = [
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
     "edc_multi_submit", "edc_multi_submit_device", "edc_multi_wait", "edc_set_slots", "edc_debug_set_scatter_stage",
+    "edc_batch_verify_prehashed", "edc_batch_verify_prehashed_device", "edc_batch_submit_prehashed",
+    "edc_batch_submit_prehashed_device", "edc_batch_verify_prehashed_fallback",
+    "edc_batch_verify_prehashed_fallback_device", "edc_multi_route", "edc_multi_debug_force_staged",
 ]
 
 
@@ -113,6 +116,20 @@ def load_library(path=None):
         lib.edc_batch_submit_indexed.argtypes = [c_vp, c_sz, ctypes.POINTER(ctypes.c_uint32), c_u8p, c_u8p, c_u64p,
                                                  c_u8p, ctypes.c_uint64, ctypes.c_int]
         lib.edc_batch_wait.argtypes = [c_vp, ctypes.c_int64, c_vp, c_vp, ctypes.POINTER(ctypes.c_int)]
+        if hasattr(lib, "edc_batch_verify_prehashed"):       # absent from older A/B builds (tools/)
+            lib.edc_batch_verify_prehashed.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_vp]
+            lib.edc_batch_verify_prehashed_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64,
+                                                              c_vp, c_vp]
+            lib.edc_batch_submit_prehashed.restype = ctypes.c_int64
+            lib.edc_batch_submit_prehashed.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u8p, ctypes.c_uint64,
+                                                       ctypes.c_int]
+            lib.edc_batch_submit_prehashed_device.restype = ctypes.c_int64
+            lib.edc_batch_submit_prehashed_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64,
+                                                              c_vp, ctypes.c_int]
+            lib.edc_batch_verify_prehashed_fallback.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u8p, c_vp,
+                                                                ctypes.POINTER(ctypes.c_int), c_vp]
+            lib.edc_batch_verify_prehashed_fallback_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_u8p, c_vp,
+                                                                       ctypes.POINTER(ctypes.c_int), c_vp]
         lib.edc_verify_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
         lib.edc_verify_each_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp]
         lib.edc_find_invalid_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, c_sz, c_vp]
@@ -140,6 +157,9 @@ def load_library(path=None):
         lib.edc_multi_submit_device.argtypes = [c_vp, ctypes.POINTER(c_sz), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                                 ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_u8p, ctypes.c_int]
         lib.edc_multi_wait.argtypes = [c_vp, ctypes.c_int64, c_vp]
+        if hasattr(lib, "edc_multi_route"):
+            lib.edc_multi_route.argtypes = [c_vp, ctypes.c_int]
+            lib.edc_multi_debug_force_staged.argtypes = [c_vp, ctypes.c_int]
         lib.edc_set_slots.argtypes = [c_vp, ctypes.c_int]
         lib.edc_verify_prehashed_each.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_vp]
         lib.edc_challenge.argtypes = [c_vp, c_sz, c_u8p, c_u8p, c_u8p, c_u64p, c_vp]
@@ -238,6 +258,43 @@ class Engine:
                                                offs, bytes(z_seed), check8)
         self._check(rc)
         return rc, (check8.raw if check8 is not None else None)
+
+    def batch_verify_prehashed(self, vks, sigs, ks, z_seed=None, z=None, want_check8=False):
+        """Batch of prehashed items {vk_bytes, sig, k} (edc_batch_verify_prehashed): the reference's
+        Verifier::verify over Items whose k was computed at Item::from (src/batch.rs:76-94)."""
+        n = len(vks)
+        check8 = ctypes.create_string_buffer(32) if want_check8 else None
+        with self._lock:
+            rc = self.lib.edc_batch_verify_prehashed(
+                self.ctx, n, b"".join(vks) or b"\0", b"".join(sigs) or b"\0", b"".join(ks) or b"\0",
+                bytes(z_seed) if z is None else None, (bytes(z) or b"\0") if z is not None else None, check8)
+        self._check(rc)
+        return rc, (check8.raw if check8 is not None else None)
+
+    def batch_submit_prehashed(self, vks, sigs, ks, z_seed, z_base=0, want_check8=False):
+        """Asynchronous prehashed batch from host buffers (edc_batch_submit_prehashed)."""
+        n = len(vks)
+        bufs = (b"".join(vks) or b"\0", b"".join(sigs) or b"\0", b"".join(ks) or b"\0", bytes(z_seed))
+        with self._lock:
+            t = self.lib.edc_batch_submit_prehashed(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], z_base,
+                                                    1 if want_check8 else 0)
+            if t < 0:
+                self._check(t)
+            self._host_inflight[t] = bufs
+        return t
+
+    def batch_verify_prehashed_fallback(self, vks, sigs, ks, z_seed):
+        """(code, per-item Item::verify_single codes, number invalid, check8) of a prehashed batch."""
+        n = len(vks)
+        check8 = ctypes.create_string_buffer(32)
+        v = ctypes.create_string_buffer(max(n, 1))
+        cnt = ctypes.c_int(0)
+        with self._lock:
+            rc = self.lib.edc_batch_verify_prehashed_fallback(self.ctx, n, b"".join(vks) or b"\0",
+                                                              b"".join(sigs) or b"\0", b"".join(ks) or b"\0",
+                                                              bytes(z_seed), v, ctypes.byref(cnt), check8)
+        self._check(rc)
+        return rc, list(v.raw[:n]), cnt.value, check8.raw
 
     def batch_submit(self, vks, sigs, msgs, z_seed, z_base=0, want_check8=False):
         """Asynchronous host-buffer batch (edc_batch_submit): returns a ticket; the staged host
@@ -446,6 +503,15 @@ class MultiEngine:
         self._check(rc)
         return rc, (check8.raw if check8 is not None else None)
 
+    def route(self, i):
+        """How shard i's result block reaches the first device: 0 local, 1 peer (xGMI), 2 host-staged."""
+        return self._check(self.lib.edc_multi_route(self.m, int(i)))
+
+    def force_staged(self, on=True):
+        """Test knob: route every shard's result block through pinned host memory (the no-peer path)."""
+        with self._lock:
+            self._check(self.lib.edc_multi_debug_force_staged(self.m, 1 if on else 0))
+
     def batch_verify_fallback(self, vks, sigs, msgs, z_seed):
         """(code, per-item verify_single codes, number invalid, check8)."""
         n = len(vks)
@@ -607,15 +673,36 @@ class batch:  # namespace mirroring `ed25519_consensus::batch`
 
         __slots__ = ("vk_bytes", "sig", "k", "_msg")
 
-        def __init__(self, vk_bytes, sig, msg, k=None):
+        def __init__(self, vk_bytes, sig, msg=None, k=None):
             self.vk_bytes = vk_bytes if isinstance(vk_bytes, VerificationKeyBytes) else VerificationKeyBytes(vk_bytes)
             self.sig = sig if isinstance(sig, Signature) else Signature(sig)
-            self._msg = bytes(msg)
-            self.k = k
+            if msg is None and k is None:
+                raise ValueError("an Item needs its message or its challenge k")
+            self._msg = bytes(msg) if msg is not None else None
+            self.k = _as_bytes(k, 32) if k is not None else None
 
         @classmethod
         def from_tuple(cls, tup):
             return cls(*tup)
+
+        @classmethod
+        def prehashed(cls, vk_bytes, sig, k):
+            """The reference's Item as it is stored, {vk_bytes, sig, k} (src/batch.rs:76-80): k was
+            computed at Item::from (e.g. by another process), the message is not needed again."""
+            return cls(vk_bytes, sig, None, k)
+
+        @staticmethod
+        def hash_many(items, engine=None):
+            """Item::from's k = H(R||A||M) mod l (src/batch.rs:82-94) for every item still without
+            one, in ONE GPU launch."""
+            eng = engine or default_engine()
+            need = [it for it in items if it.k is None]
+            if need:
+                ks = eng.challenge([it.vk_bytes.to_bytes() for it in need], [it.sig.to_bytes() for it in need],
+                                   [it._msg for it in need])
+                for it, k in zip(need, ks):
+                    it.k = k
+            return items
 
         def verify_single(self, engine=None):
             eng = engine or default_engine()
@@ -629,12 +716,7 @@ class batch:  # namespace mirroring `ed25519_consensus::batch`
         def verify_single_many(items, engine=None):
             """Fallback for many items in ONE GPU launch; returns per-item verdict codes."""
             eng = engine or default_engine()
-            need = [it for it in items if it.k is None]
-            if need:
-                ks = eng.challenge([it.vk_bytes.to_bytes() for it in need], [it.sig.to_bytes() for it in need],
-                                   [it._msg for it in need])
-                for it, k in zip(need, ks):
-                    it.k = k
+            batch.Item.hash_many(items, eng)
             return eng.verify_prehashed_each([it.vk_bytes.to_bytes() for it in items],
                                              [it.sig.to_bytes() for it in items], [it.k for it in items])
 
@@ -644,7 +726,7 @@ class batch:  # namespace mirroring `ed25519_consensus::batch`
 
         def __init__(self, engine=None):
             self._engine = engine
-            self._vks, self._sigs, self._msgs = [], [], []
+            self._vks, self._sigs, self._msgs, self._ks = [], [], [], []
 
         @classmethod
         def new(cls, engine=None):
@@ -662,22 +744,32 @@ class batch:  # namespace mirroring `ed25519_consensus::batch`
             self._vks.append(item.vk_bytes.to_bytes())
             self._sigs.append(item.sig.to_bytes())
             self._msgs.append(item._msg)
+            self._ks.append(item.k)
 
         def verify_detailed(self, rng=None):
             """Returns (code, check8): check8 = compressed [8]*check (None when rejected before
             the MSM). rng: a 32-byte ChaCha20 seed, an object with fill_bytes(n)/token_bytes(n),
-            or None (fresh OS randomness)."""
+            or None (fresh OS randomness). Items that carry their k (prehashed, as the reference's
+            Item always does) go through edc_batch_verify_prehashed; otherwise SHA-512 runs on the
+            GPU inside the batch."""
             eng = self._engine or default_engine()
             n = len(self._vks)
             if isinstance(rng, (bytes, bytearray)) and len(rng) == 32:
-                return eng.batch_verify(self._vks, self._sigs, self._msgs, z_seed=bytes(rng), want_check8=True)
-            if rng is None:
-                return eng.batch_verify(self._vks, self._sigs, self._msgs, z_seed=secrets.token_bytes(32),
-                                        want_check8=True)
-            # gen_u128 per item in queue order (src/batch.rs:64-68)
-            draw = rng.fill_bytes if hasattr(rng, "fill_bytes") else rng.token_bytes
-            z = b"".join(bytes(draw(16)) for _ in range(n))
-            return eng.batch_verify(self._vks, self._sigs, self._msgs, z=z, want_check8=True)
+                zkw = {"z_seed": bytes(rng)}
+            elif rng is None:
+                zkw = {"z_seed": secrets.token_bytes(32)}
+            else:   # gen_u128 per item in queue order (src/batch.rs:64-68)
+                draw = rng.fill_bytes if hasattr(rng, "fill_bytes") else rng.token_bytes
+                zkw = {"z": b"".join(bytes(draw(16)) for _ in range(n))}
+            if any(m is None for m in self._msgs) or (n and all(k is not None for k in self._ks)):
+                if any(k is None for k in self._ks):     # mixed queue: hash the rest in one launch
+                    need = [i for i, k in enumerate(self._ks) if k is None]
+                    ks = eng.challenge([self._vks[i] for i in need], [self._sigs[i] for i in need],
+                                       [self._msgs[i] for i in need])
+                    for i, k in zip(need, ks):
+                        self._ks[i] = k
+                return eng.batch_verify_prehashed(self._vks, self._sigs, self._ks, want_check8=True, **zkw)
+            return eng.batch_verify(self._vks, self._sigs, self._msgs, want_check8=True, **zkw)
 
         def verify(self, rng=None):
             """Verifier::verify: returns None on success, raises InvalidSignature otherwise."""

@@ -52,6 +52,8 @@ struct Slot {
   hipStream_t st = nullptr;
   size_t cap_n = 0, cap_T = 0;
   uint32_t *k = nullptr, *key_slot = nullptr, *key_index = nullptr, *key_rep = nullptr;
+  // the batch's challenges: k (computed by k_challenge) or a prehashed caller's device array
+  const uint32_t* kin = nullptr;
   uint32_t *table = nullptr, *slot_key = nullptr;
   uint32_t *pts = nullptr, *scal = nullptr;
   unsigned long long *key_acc = nullptr, *u_acc = nullptr;
@@ -127,6 +129,8 @@ struct edc_ctx {
   uint8_t* fb_rv = nullptr;      // per-range verdict | pre-bad flag
   uint32_t* fb_idx = nullptr;    // items verified one by one
   size_t fb_cap_idx = 0;
+  uint8_t* fb_g = nullptr;       // their gathered vk | sig | k (fb_cap_g items each)
+  size_t fb_cap_g = 0;
   uint32_t fb_ranges = 32;      // target range count of the grouped fallback
   int fb_bits = 10;             // its window width
   // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
@@ -495,13 +499,9 @@ static int upload(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
 
 // Stage host inputs into slot s's own device buffers on the slot's stream (edc_batch_submit), so
 // the copy of one batch overlaps the kernels of the batches already in flight on other slots.
-static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
-                       const uint64_t* msg_off, const uint32_t* key_idx = nullptr) {
-  if (n && ((!vk && !key_idx) || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+static int ensure_slot_inputs(edc_ctx* ctx, Slot& s, size_t n, size_t mbytes) {
   int rc = init_slot(ctx, s);
   if (rc) return rc;
-  const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
-  if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
   if (n > s.in_cap_n || !s.in_vk) {
     CK(hipStreamSynchronize(s.st));
     void* in[] = {s.in_vk, s.in_sig, s.in_off, s.in_idx};
@@ -527,6 +527,16 @@ static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const
     CK(dalloc(&s.in_msg, cap));
     s.in_cap_msg = cap;
   }
+  return 0;
+}
+
+static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                       const uint64_t* msg_off, const uint32_t* key_idx = nullptr) {
+  if (n && ((!vk && !key_idx) || !sig || !msg_off)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+  const size_t mbytes = n ? (size_t)(msg_off[n] - msg_off[0]) : 0;
+  if (mbytes && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
+  int rc = ensure_slot_inputs(ctx, s, n, mbytes);
+  if (rc) return rc;
   if (!n) return 0;
   hipStream_t st = s.st;
   const uint64_t* off = msg_off;
@@ -548,6 +558,25 @@ static int upload_slot(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const
   return 0;
 }
 
+// Prehashed host submissions (reference Item = {vk_bytes, sig, k}, src/batch.rs:76-80): keys and
+// signatures into the slot's input buffers, the 32-byte challenges straight into the slot's k
+// array (128 B per item over PCIe, no message bytes).
+static int upload_slot_prehashed(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* vk, const uint8_t* sig,
+                                 const uint8_t* k) {
+  if (n && (!vk || !sig || !k)) { ctx->err = "null input"; return EDC_ERR_ARG; }
+  int rc = ensure_slot_inputs(ctx, s, n, 0);
+  if (rc) return rc;
+  rc = ensure_slot(ctx, s, n);
+  if (rc || !n) return rc;
+  CK(hipMemcpyAsync(s.in_vk, vk, n * 32, hipMemcpyHostToDevice, s.st));
+  CK(hipMemcpyAsync(s.in_sig, sig, n * 64, hipMemcpyHostToDevice, s.st));
+  CK(hipMemcpyAsync(s.k, k, n * 32, hipMemcpyHostToDevice, s.st));
+  return 0;
+}
+
+// caller-supplied device k arrays are read with 16-byte loads
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
 static uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -566,14 +595,21 @@ static bool choose_per_sig(const edc_ctx* ctx, size_t n) {
 }
 
 // Enqueue the per-signature prefix of the pipeline on slot s: key grouping, SHA-512 challenges,
-// z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization.
+// z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization. With d_k (the
+// prehashed entries: the caller's queue-time k, src/batch.rs:76-94) SHA-512 is skipped and the
+// messages are not read (d_msg / d_off may be null).
 static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
                           const uint8_t* d_z, bool with_bin, const MsmPlan* P, bool force_per_sig = false,
-                          bool split = false) {
+                          bool split = false, const uint32_t* d_k = nullptr) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
+  if (n && (!aligned16(d_vk) || !aligned16(d_sig) || (d_z && !aligned16(d_z)) || (d_k && !aligned16(d_k)))) {
+    ctx->err = "device vk / sig / z / k arrays must be 16-byte aligned";
+    return EDC_ERR_ARG;
+  }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
+  s.kin = d_k ? d_k : s.k;
   const uint32_t N = (uint32_t)n;
   const uint32_t T = (uint32_t)next_pow2(2 * (n < 128 ? 128 : n));
   if (T > s.cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
@@ -598,7 +634,14 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   }
   // dual-stream builds (untimed batches): the decode only needs the key grouping, so it runs on
   // the slot's second stream beside SHA-512 / coefficients / binning; its per-item R bits go to
-  // their own array (itembad + cap_n), so no byte is written by both streams
+  // their own array (itembad + cap_n), so no byte is written by both streams.
+  // Contract while st2 runs (between ev_keys and the wait on ev_dec below): k_decompress reads
+  // d_sig, d_vk, key_rep, flags[FLAG_NKEYS / FLAG_OVF] and the key cache, and writes pts,
+  // itembad + cap_n, keybad and flags[FLAG_BAD / FLAG_UNCACHED] (atomics). The kernels enqueued on
+  // st in between (challenge, coefficients, binning) must not read pts / keybad / itembad + cap_n,
+  // write key_rep or FLAG_NKEYS / FLAG_OVF, or plain-store into flags; anything that does must
+  // come after the ev_dec wait. tests/test_gpu_prehashed.py compares slot 0 (dual stream) with a
+  // pipelined slot (one stream) on batches that fail in the decode and in the s check.
   const bool dual = EDC_DUAL_STREAM && s.st2 && !s.timed;
   if (dual) {
     CK(hipEventRecord(s.ev_keys, st));
@@ -609,9 +652,9 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
     CK(hipEventRecord(s.ev_dec, s.st2));
   }
   mark(PH_CHALLENGE);
-  if (EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
+  if (!d_k && EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
-  if (EDC_RUN(4)) launch_coef(st, N, d_sig, s.k, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
+  if (EDC_RUN(4)) launch_coef(st, N, d_sig, s.kin, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
               per_sig, s.coef_part, split);
   mark(PH_MSM_BIN);
   if (with_bin && EDC_RUN(8))
@@ -631,7 +674,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
 // Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
 static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                          const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
-                         const uint8_t* d_z, int want_compress) {
+                         const uint8_t* d_z, int want_compress, const uint32_t* d_k = nullptr) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
@@ -639,7 +682,7 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   const MsmPlan P = batch_plan(ctx, n, per_sig, split);
   rc = ensure_msm(ctx, s, P, split ? msm_entry_capacity(P, 2 + 3 * n, 0) : msm_entry_capacity(P, n, n + 1));
   if (rc) return rc;
-  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P, per_sig, split);
+  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P, per_sig, split, d_k);
   if (rc) return rc;
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
@@ -676,6 +719,10 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
     }
     if (ctx->kc_m) ctx->last_uncached = (uint32_t)reinterpret_cast<int*>(s.h_out)[44];
   }
+  if (&s != &ctx->comb && reinterpret_cast<int*>(s.h_out)[45]) {
+    ctx->err = "prehashed k is not a canonical scalar (must be < l, as Scalar::from_hash returns)";
+    return EDC_ERR_ARG;
+  }
   if (check8) {
     if (bad) memset(check8, 0, 32);
     else memcpy(check8, s.h_out + 16, 32);
@@ -688,10 +735,10 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
 // Synchronous batch on slot 0.
 static int run_batch_sync(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig, const uint8_t* d_msg,
                           const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base, const uint8_t* d_z,
-                          uint8_t check8[32], uint8_t partial[128], int* bad) {
+                          uint8_t check8[32], uint8_t partial[128], int* bad, const uint32_t* d_k = nullptr) {
   Slot& s = ctx->slot[0];
   if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
-  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, check8 != nullptr);
+  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, check8 != nullptr, d_k);
   if (rc) return rc;
   return finish_batch(ctx, s, check8, partial, bad);
 }
@@ -778,7 +825,8 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
-                  ctx->btab, ctx->comb_in, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal, ctx->fb_rv, ctx->fb_idx};
+                  ctx->btab, ctx->comb_in, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal, ctx->fb_rv, ctx->fb_idx,
+                  ctx->fb_g};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete ctx;
@@ -1015,14 +1063,27 @@ static int verify_listed(edc_ctx* ctx, Slot& s, const std::vector<uint32_t>& idx
     CK(dalloc(&ctx->fb_idx, c + c / 8 + 64));
     ctx->fb_cap_idx = c + c / 8 + 64;
   }
+  // gathered copies in their own buffer: the inputs may BE the context's staging buffers (host
+  // entry points), and an in-place gather would race (item idx[j] > j is read while slot idx[j]
+  // is written by another lane)
+  if (c > ctx->fb_cap_g || !ctx->fb_g) {
+    if (ctx->fb_g) (void)hipFree(ctx->fb_g);
+    ctx->fb_g = nullptr;
+    ctx->fb_cap_g = 0;
+    CK(dalloc(&ctx->fb_g, (c + c / 8 + 64) * 128));
+    ctx->fb_cap_g = c + c / 8 + 64;
+  }
+  uint8_t* g_vk = ctx->fb_g;
+  uint8_t* g_sig = g_vk + ctx->fb_cap_g * 32;
+  uint32_t* g_k = reinterpret_cast<uint32_t*>(g_sig + ctx->fb_cap_g * 64);
   hipStream_t st = s.st;
   CK(hipMemcpyAsync(ctx->fb_idx, idx.data(), c * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  launch_gather_items(st, (uint32_t)c, ctx->fb_idx, d_vk, d_sig, s.k, ctx->vk, ctx->sig, ctx->kbuf);
+  launch_gather_items(st, (uint32_t)c, ctx->fb_idx, d_vk, d_sig, s.kin, g_vk, g_sig, g_k);
   if (c <= kQuadVerifyMax)   // latency-bound: one quad of lanes per item
-    launch_verify_quad(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->verdicts, ctx->kc(), ctx->bcomb);
+    launch_verify_quad(st, (uint32_t)c, g_vk, g_sig, g_k, ctx->btab, ctx->verdicts, ctx->kc(), ctx->bcomb);
   else
-    launch_verify_single(st, (uint32_t)c, ctx->vk, ctx->sig, ctx->kbuf, ctx->btab, ctx->vtab, ctx->verdicts,
-                         ctx->kc(), ctx->bcomb);
+    launch_verify_single(st, (uint32_t)c, g_vk, g_sig, g_k, ctx->btab, ctx->vtab, ctx->verdicts, ctx->kc(),
+                         ctx->bcomb);
   CK(hipGetLastError());
   std::vector<uint8_t> v(c);
   CK(hipMemcpyAsync(v.data(), ctx->verdicts, c, hipMemcpyDeviceToHost, st));
@@ -1058,7 +1119,9 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   if (!per_sig && (size_t)G * m > s.cap_n) {
     // too many distinct keys for per-(range, key) sums: redo the prefix with one key term per
     // signature (the same group element)
-    int rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, nullptr, false, nullptr, true);
+    // (s.kin already holds this batch's k: computed by the first prefix or the caller's)
+    int rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, nullptr, false, nullptr, true, false,
+                            s.kin);
     if (rc) return rc;
     CK(hipStreamSynchronize(s.st));
     per_sig = true;
@@ -1074,7 +1137,7 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   uint32_t seed[8];
   seed_words(z_seed, seed);
   hipStream_t st = s.st;
-  launch_range_coef(st, (uint32_t)n, (uint32_t)rsize, G, m, per_sig, d_sig, s.k, nullptr, seed, z_base, s.key_index,
+  launch_range_coef(st, (uint32_t)n, (uint32_t)rsize, G, m, per_sig, d_sig, s.kin, nullptr, seed, z_base, s.key_index,
                     s.scal, s.key_acc, s.u_acc, s.flags, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal);
   const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
                        ctx->fb_xscal};
@@ -1127,13 +1190,14 @@ int edc_find_invalid_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
   return fallback_ranges(ctx, s, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, per_sig, m, verdicts);
 }
 
-int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
-                                     const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
-                                     uint8_t* verdicts, int* n_invalid, uint8_t check8[32]) {
-  if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_msg_off || !verdicts))) return EDC_ERR_ARG;
-  CK(hipSetDevice(ctx->device));
+}  // extern "C"
+
+// batch on slot 0, then (on failure) the grouped fallback reusing its state; d_k: prehashed k
+static int batch_with_fallback(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig, const uint8_t* d_msg,
+                               const uint64_t* d_msg_off, const uint32_t* d_k, const uint8_t* z_seed,
+                               uint8_t* verdicts, int* n_invalid, uint8_t check8[32]) {
   if (n_invalid) *n_invalid = 0;
-  int rc = run_batch_sync(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, nullptr, check8, nullptr, nullptr);
+  int rc = run_batch_sync(ctx, n, d_vk, d_sig, d_msg, d_msg_off, z_seed, 0, nullptr, check8, nullptr, nullptr, d_k);
   if (rc <= 0) {
     if (rc == 0 && n) memset(verdicts, 0, n);
     return rc;
@@ -1147,6 +1211,110 @@ int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk
   if (r2 < 0) return r2;
   if (n_invalid) *n_invalid = r2;
   return EDC_INVALID_SIGNATURE;
+}
+
+extern "C" {
+
+int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                     const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t z_seed[32],
+                                     uint8_t* verdicts, int* n_invalid, uint8_t check8[32]) {
+  if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_msg_off || !verdicts))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  return batch_with_fallback(ctx, n, d_vk, d_sig, d_msg, d_msg_off, nullptr, z_seed, verdicts, n_invalid, check8);
+}
+
+// ---- prehashed items: the reference's batch::Item {vk_bytes, sig, k} (src/batch.rs:76-94) ----
+int edc_batch_verify_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* k,
+                               const uint8_t z_seed[32], const uint8_t* z, uint8_t check8[32]) {
+  if (!ctx || (!z_seed && !z) || (n && (!vk || !sig || !k || (!z_seed && !z)))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
+  int rc = ensure_n(ctx, n);
+  if (rc) return rc;
+  rc = ensure_slot(ctx, s, n);
+  if (rc) return rc;
+  hipStream_t st = ctx->st();
+  if (n) {
+    CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(s.k, k, n * 32, hipMemcpyHostToDevice, st));
+    if (z) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, st));
+  }
+  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, nullptr, nullptr, z ? nullptr : z_seed, 0, z ? ctx->zexp : nullptr,
+                        check8, nullptr, nullptr, s.k);
+}
+
+int edc_batch_verify_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                      const uint8_t* d_k, const uint8_t z_seed[32], uint64_t z_base,
+                                      const uint8_t* d_z, uint8_t check8[32]) {
+  if (!ctx || (!z_seed && !d_z) || (n && (!d_vk || !d_sig || !d_k))) return EDC_ERR_ARG;
+  if (!aligned16(d_k) || (d_z && !aligned16(d_z))) { ctx->err = "d_k / d_z must be 16-byte aligned"; return EDC_ERR_ARG; }
+  CK(hipSetDevice(ctx->device));
+  return run_batch_sync(ctx, n, d_vk, d_sig, nullptr, nullptr, z_seed, z_base, d_z, check8, nullptr, nullptr,
+                        reinterpret_cast<const uint32_t*>(d_k));
+}
+
+int64_t edc_batch_submit_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* k,
+                                   const uint8_t z_seed[32], uint64_t z_base, int want_check8) {
+  if (!ctx || !z_seed) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % ctx->nslots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = upload_slot_prehashed(ctx, s, n, vk, sig, k);
+  if (rc) return rc;
+  rc = enqueue_batch(ctx, s, n, s.in_vk, s.in_sig, nullptr, nullptr, z_seed, z_base, nullptr, want_check8 != 0, s.k);
+  if (rc) return rc;
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int64_t edc_batch_submit_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                          const uint8_t* d_k, const uint8_t z_seed[32], uint64_t z_base,
+                                          const uint8_t* d_z, int want_check8) {
+  if (!ctx || (!z_seed && !d_z) || (n && (!d_vk || !d_sig || !d_k))) return EDC_ERR_ARG;
+  if (!aligned16(d_k) || (d_z && !aligned16(d_z))) { ctx->err = "d_k / d_z must be 16-byte aligned"; return EDC_ERR_ARG; }
+  CK(hipSetDevice(ctx->device));
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % ctx->nslots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, nullptr, nullptr, z_seed, z_base, d_z, want_check8 != 0,
+                         reinterpret_cast<const uint32_t*>(d_k));
+  if (rc) return rc;
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int edc_batch_verify_prehashed_fallback(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                                        const uint8_t* k, const uint8_t z_seed[32], uint8_t* verdicts,
+                                        int* n_invalid, uint8_t check8[32]) {
+  if (!ctx || !z_seed || (n && (!vk || !sig || !k || !verdicts))) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
+  int rc = ensure_n(ctx, n);
+  if (rc) return rc;
+  rc = ensure_slot(ctx, s, n);
+  if (rc) return rc;
+  if (n) {
+    CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st()));
+    CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st()));
+    CK(hipMemcpyAsync(s.k, k, n * 32, hipMemcpyHostToDevice, ctx->st()));
+  }
+  return batch_with_fallback(ctx, n, ctx->vk, ctx->sig, nullptr, nullptr, s.k, z_seed, verdicts, n_invalid, check8);
+}
+
+int edc_batch_verify_prehashed_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                               const uint8_t* d_k, const uint8_t z_seed[32], uint8_t* verdicts,
+                                               int* n_invalid, uint8_t check8[32]) {
+  if (!ctx || !z_seed || (n && (!d_vk || !d_sig || !d_k || !verdicts))) return EDC_ERR_ARG;
+  if (!aligned16(d_k)) { ctx->err = "d_k must be 16-byte aligned"; return EDC_ERR_ARG; }
+  CK(hipSetDevice(ctx->device));
+  return batch_with_fallback(ctx, n, d_vk, d_sig, nullptr, nullptr, reinterpret_cast<const uint32_t*>(d_k), z_seed,
+                             verdicts, n_invalid, check8);
 }
 
 int edc_decompress(edc_ctx* ctx, size_t n, const uint8_t* enc, uint8_t* xy, uint8_t* ok) {
@@ -1406,11 +1574,18 @@ int edc_synchronize(edc_ctx* ctx) {
 // partials are gathered through the host (they already come back with each shard's verdict) and
 // summed on the first device, then x8 and the identity test. One host thread per device drives
 // its shard; the same device may appear several times (several contexts on one GPU).
-// One in-flight multi-device batch (edc_multi_submit): every shard's 256-byte result block is
-// copied device to device (a peer store over xGMI by a one-wave kernel on the shard's stream; a
-// plain copy when a device is listed twice) into
-// `blocks` on the first device, whose combine stream waits for every shard's copy event and sums
-// the partial points there (k_combine_blocks). The host only enqueues, and waits once per batch.
+// One in-flight multi-device batch (edc_multi_submit): every shard's 256-byte result block reaches
+// `blocks` on the first device, whose combine stream waits for every shard's event and sums the
+// partial points there (k_combine_blocks). The host only enqueues, and waits once per batch. How a
+// block travels depends on the pair (edc_multi.route, fixed at edc_create_multi):
+//  - ROUTE_LOCAL: the shard runs on the first device itself (listed twice): a one-wave kernel on
+//    the shard's stream copies it;
+//  - ROUTE_PEER: peer access from the shard's device to the first device was enabled: the same
+//    kernel stores it over xGMI;
+//  - ROUTE_STAGED: no peer access (or forced by edc_multi_debug_force_staged): the shard's final
+//    kernel already wrote the block to its slot's pinned host mirror; the combine stream waits for
+//    the shard's event and copies that mirror to `blocks` itself. No kernel ever stores to another
+//    device's memory without peer access enabled.
 struct MultiSlot {
   bool pending = false;
   int64_t ticket = -1;
@@ -1423,10 +1598,15 @@ struct MultiSlot {
   uint8_t* h_out = nullptr;          // pinned mirror
 };
 
+enum { ROUTE_LOCAL = 0, ROUTE_PEER = 1, ROUTE_STAGED = 2 };
+
 struct edc_multi {
   std::vector<edc_ctx*> ctx;
+  std::vector<int> route;            // per shard: ROUTE_LOCAL / ROUTE_PEER / ROUTE_STAGED
+  std::vector<int> route_auto;       // as found by edc_create_multi (edc_multi_debug_force_staged(0) restores it)
   std::string err;
   MultiSlot ms[kSlots];
+  int ring = kSlots;                 // multi-batches in flight = the smallest shard context's slot count
   int64_t next_ticket = 0;
   hipStream_t comb = nullptr;        // first device: every batch's combine, in submission order
 };
@@ -1497,6 +1677,11 @@ static int multi_batch(edc_multi* M, size_t n, const uint8_t* vk, const uint8_t*
   } while (0)
 
 static int multi_slot_init(edc_multi* M, MultiSlot& ms) {
+  for (edc_ctx* c : M->ctx)
+    if (c->nslots < M->ring) {   // edc_set_slots on a shard context after edc_create_multi
+      M->err = "a shard context has fewer in-flight slots than the multi-device ring";
+      return EDC_ERR_ARG;
+    }
   if (ms.done) return 0;
   const size_t g = M->ctx.size();
   MCK(hipSetDevice(M->ctx[0]->device));
@@ -1535,11 +1720,17 @@ static int multi_link_shard(edc_multi* M, MultiSlot& ms, size_t g, int64_t t) {
   Slot& s = c->slot[t % c->nslots];
   if (!s.pending || s.ticket != t || !s.d_out) { M->err = "shard ticket has no pending slot"; return EDC_ERR_ARG; }
   MCK(hipSetDevice(c->device));
-  launch_copy_block(s.st, s.d_out, ms.blocks + 256 * g);   // hipMemcpyPeerAsync blocks the host here
-  MCK(hipGetLastError());
+  const int route = M->route[g];
+  if (route != ROUTE_STAGED) {
+    launch_copy_block(s.st, s.d_out, ms.blocks + 256 * g);   // hipMemcpyPeerAsync blocks the host here
+    MCK(hipGetLastError());
+  }
   MCK(hipEventRecord(ms.copied[g], s.st));
   MCK(hipSetDevice(M->ctx[0]->device));
   MCK(hipStreamWaitEvent(M->comb, ms.copied[g], 0));
+  // staged: the shard's final kernel stored its block to the slot's pinned host mirror (the slot is
+  // not reused before edc_multi_wait has synchronized this combine)
+  if (route == ROUTE_STAGED) MCK(hipMemcpyAsync(ms.blocks + 256 * g, s.h_out, 256, hipMemcpyHostToDevice, M->comb));
   return 0;
 }
 
@@ -1580,24 +1771,51 @@ edc_multi* edc_create_multi(const int* devices, int ndev) {
     }
     M->ctx.push_back(c);
   }
-  // contexts sharing one GPU split its eight in-flight slots (one hardware queue each), so that a
-  // rehearsal with a device listed several times does not oversubscribe the queue scheduler
+  // contexts sharing one GPU split its kSlots (16) in-flight slots (one hardware queue each), so
+  // that a rehearsal with a device listed several times does not oversubscribe the queue scheduler;
+  // the multi-batch ring is the smallest share, so a multi submission never finds a shard's slot busy
+  M->ring = kSlots;
   for (int i = 0; i < ndev; ++i) {
     int same = 0;
     for (int j = 0; j < ndev; ++j) same += devices[j] == devices[i];
     M->ctx[i]->nslots = kSlots / same > 0 ? kSlots / same : 1;
+    if (M->ctx[i]->nslots < M->ring) M->ring = M->ctx[i]->nslots;
   }
-  // direct xGMI copies of the shards' result blocks to the first device (edc_multi_submit)
+  // how each shard's result block reaches the first device (edc_multi_submit): a peer store over
+  // xGMI only where peer access from the shard's device to the first device is actually enabled;
+  // any other outcome of the enable than success / already-enabled is an error
+  M->route.assign(ndev, ROUTE_LOCAL);
   for (int i = 1; i < ndev; ++i) {
     if (devices[i] == devices[0]) continue;
     int can = 0;
-    if (hipDeviceCanAccessPeer(&can, devices[0], devices[i]) == hipSuccess && can) {
-      (void)hipSetDevice(devices[i]);
-      (void)hipDeviceEnablePeerAccess(devices[0], 0);   // already enabled is fine
+    if (hipDeviceCanAccessPeer(&can, devices[i], devices[0]) != hipSuccess || !can) {
       (void)hipGetLastError();
+      M->route[i] = ROUTE_STAGED;
+      continue;
     }
+    const hipError_t e = hipSetDevice(devices[i]) == hipSuccess ? hipDeviceEnablePeerAccess(devices[0], 0)
+                                                                 : hipErrorInvalidDevice;
+    (void)hipGetLastError();
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+      edc_destroy_multi(M);
+      return nullptr;
+    }
+    M->route[i] = ROUTE_PEER;
   }
+  M->route_auto = M->route;
   return M;
+}
+
+int edc_multi_debug_force_staged(edc_multi* M, int on) {
+  if (!M) return EDC_ERR_ARG;
+  for (const MultiSlot& ms : M->ms)
+    if (ms.pending) { M->err = "route change with a batch in flight"; return EDC_ERR_ARG; }
+  for (size_t i = 0; i < M->ctx.size(); ++i) M->route[i] = on ? (int)ROUTE_STAGED : M->route_auto[i];
+  return 0;
+}
+
+int edc_multi_route(const edc_multi* M, int i) {
+  return (M && i >= 0 && i < (int)M->route.size()) ? M->route[i] : EDC_ERR_ARG;
 }
 
 void edc_destroy_multi(edc_multi* M) {
@@ -1615,7 +1833,7 @@ int64_t edc_multi_submit(edc_multi* M, size_t n, const uint8_t* vk, const uint8_
                          const uint64_t* msg_off, const uint8_t z_seed[32], int want_check8) {
   if (!M || !z_seed || (n && (!vk || !sig || !msg_off))) return EDC_ERR_ARG;
   const int64_t ticket = M->next_ticket;
-  MultiSlot& ms = M->ms[ticket % kSlots];
+  MultiSlot& ms = M->ms[ticket % M->ring];
   if (ms.pending) { M->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = multi_slot_init(M, ms);
   if (rc) return rc;
@@ -1639,7 +1857,7 @@ int64_t edc_multi_submit_device(edc_multi* M, const size_t* n, const uint8_t* co
                                 const uint8_t z_seed[32], int want_check8) {
   if (!M || !z_seed || !n || !d_vk || !d_sig || !d_msg || !d_msg_off) return EDC_ERR_ARG;
   const int64_t ticket = M->next_ticket;
-  MultiSlot& ms = M->ms[ticket % kSlots];
+  MultiSlot& ms = M->ms[ticket % M->ring];
   if (ms.pending) { M->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
   int rc = multi_slot_init(M, ms);
   if (rc) return rc;
@@ -1661,7 +1879,7 @@ int64_t edc_multi_submit_device(edc_multi* M, const size_t* n, const uint8_t* co
 
 int edc_multi_wait(edc_multi* M, int64_t ticket, uint8_t check8[32]) {
   if (!M || ticket < 0) return EDC_ERR_ARG;
-  MultiSlot& ms = M->ms[ticket % kSlots];
+  MultiSlot& ms = M->ms[ticket % M->ring];
   if (!ms.pending || ms.ticket != ticket) { M->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
   ms.pending = false;
   int err = 0;
@@ -1672,8 +1890,12 @@ int edc_multi_wait(edc_multi* M, int64_t ticket, uint8_t check8[32]) {
       M->err = std::string("device ") + std::to_string(M->ctx[g]->device) + ": " + edc_last_error(M->ctx[g]);
     }
   }
-  if (err) return err;
   MCK(hipSetDevice(M->ctx[0]->device));
+  if (err) {   // the combine may still be running on M->comb: drain it before the slot can be reused
+    (void)hipEventSynchronize(ms.done);
+    (void)hipGetLastError();
+    return err;
+  }
   MCK(hipEventSynchronize(ms.done));
   const int verdict = reinterpret_cast<int*>(ms.h_out)[0];
   const int bad = reinterpret_cast<int*>(ms.h_out)[1];

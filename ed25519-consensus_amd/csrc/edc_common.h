@@ -130,7 +130,9 @@ constexpr int KEY_ACC_LIMBS = 12;
 // DESIGN.md): the batch continues with one key term per signature, which is the same group element.
 // FLAG_UNCACHED: keys of the batch not found in the context's key cache (reported to the host,
 // which only plans split coefficients while the previous batch had none).
-enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_UNCACHED = 4, FLAG_COUNT = 8 };
+// FLAG_KARG: a caller-supplied challenge k (prehashed entries) was not a canonical scalar (>= l):
+// a broken caller contract, reported as EDC_ERR_ARG, never as a verdict.
+enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_UNCACHED = 4, FLAG_KARG = 5, FLAG_COUNT = 8 };
 
 // Points of a batch MSM: 0 = B, 1..n = R_i, n+1..n+m = the distinct keys (grouped) or each
 // signature's own key (m = n, one key term per signature).

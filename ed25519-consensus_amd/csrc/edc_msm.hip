@@ -782,6 +782,7 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
     blk[2] = (uint32_t)flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
     blk[3] = (uint32_t)flags[FLAG_OVF];
     blk[44] = (uint32_t)flags[FLAG_UNCACHED];   // byte 176, after the partial point
+    blk[45] = (uint32_t)flags[FLAG_KARG];       // byte 180: a caller's k was not canonical
     if (want_compress) ge_compress(c8, blk + 4);   // bytes 16..48 (little-endian words)
   }
   __syncthreads();

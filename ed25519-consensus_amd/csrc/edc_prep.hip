@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
   unsigned long long ua[PL];
 #pragma unroll
   for (int j = 0; j < PL; ++j) ua[j] = 0;
-  bool bad = false;
+  bool bad = false, karg = false;
   const uint32_t base = blockIdx.x * COEF_CHUNK;
   const uint32_t pair0 = rsize ? (base / rsize) * m : 0u;
   for (int grp = 0; grp < COEF_SIGS_PER_THREAD / 4; ++grp) {
@@ -342,6 +342,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
       kw[0] = k0.x; kw[1] = k0.y; kw[2] = k0.z; kw[3] = k0.w; kw[4] = k1.x; kw[5] = k1.y; kw[6] = k1.z; kw[7] = k1.w;
       const bool s_bad = !sc_is_canonical(sw);
       bad |= s_bad;
+      karg |= !sc_is_canonical(kw);   // k from Scalar::from_hash is < l; only a prehashed caller can break it
       if (!rsize) itembad[i] = s_bad ? ITEM_BAD_S : 0;   // first writer of the batch's per-item bits
       uint32_t u[PL], v[PL];
       mul_128x256(z, sw, u);
@@ -381,6 +382,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
     }
   }
   if (bad) atomicOr(&flags[FLAG_BAD], 1);
+  if (karg) atomicOr(&flags[FLAG_KARG], 1);
   // workgroup reduction of the per-thread z*s limb sums (64-bit shuffles, then LDS)
 #pragma unroll
   for (int j = 0; j < PL; ++j) {

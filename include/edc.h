@@ -11,6 +11,10 @@
  *  - Host buffers are borrowed for the duration of the call; all calls are synchronous.
  *  - Items are in QUEUE order. vk: n*32 bytes, sig: n*64 bytes (R || s), messages are one
  *    arena `msg` with n+1 offsets (message i = msg[msg_off[i] .. msg_off[i+1])).
+ *  - Device-resident inputs (the *_device entries): vk / sig / k arrays 16-byte aligned; the
+ *    message arena may be read up to the next 4-byte boundary after the last message byte (the
+ *    SHA-512 kernel loads whole aligned dwords), so that many bytes past it must be mapped. Device
+ *    allocations (hipMalloc, torch tensors) always satisfy both; host buffers have no such rule.
  *  - z_i = u128::from_le_bytes(ChaCha20Rng::from_seed(z_seed) keystream[16(z_base+i) ..]),
  *    i.e. gen_u128 (reference src/batch.rs:64-68) drawn in queue order. Batch verification is
  *    sound only when z is unpredictable to the signers: z_seed must come from a CSPRNG, fresh for
@@ -177,6 +181,41 @@ int edc_batch_verify_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk
                                      uint8_t* verdicts, int* n_invalid, uint8_t check8[32]);
 
 /*
+ * Prehashed batches: the reference's batch::Item is {vk_bytes, sig, k} (src/batch.rs:76-80) --
+ * k = H(R||A||M) mod l is computed once, at Item::from (src/batch.rs:82-94), and
+ * Verifier::queue / verify (src/batch.rs:127-137, :149-217) never see the message again. These
+ * entries take that k (n*32 bytes, queue order, canonical little-endian scalars < l, as
+ * Scalar::from_hash returns) instead of the message arena: SHA-512 is skipped and only
+ * 32 + 64 + 32 bytes per item are read. Everything downstream is the message path's pipeline, so
+ * verdicts and check8 are bit-identical to edc_batch_verify on the messages those k came from.
+ * A k >= l is a broken caller contract: the call returns EDC_ERR_ARG (never a verdict).
+ *  - edc_batch_verify_prehashed: host buffers, synchronous; z from z_seed (ChaCha20, as
+ *    edc_batch_verify) or, when z_seed is NULL, caller-drawn z (n*16 bytes, LE u128 per item).
+ *  - edc_batch_verify_prehashed_device: device buffers; z as edc_batch_verify_device.
+ *  - edc_batch_submit_prehashed / _device: asynchronous forms (edc_batch_submit /
+ *    edc_batch_submit_device rules; waited with edc_batch_wait). Inputs are borrowed until the wait.
+ *  - edc_batch_verify_prehashed_fallback[_device]: the batch and, if it fails, the grouped fallback
+ *    of edc_batch_verify_fallback_device (verdicts[i] = Item::verify_single's code, src/batch.rs:104-107).
+ * Device k / z arrays must be 16-byte aligned (EDC_ERR_ARG otherwise).
+ */
+int edc_batch_verify_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* k,
+                               const uint8_t z_seed[32], const uint8_t* z, uint8_t check8[32]);
+int edc_batch_verify_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                      const uint8_t* d_k, const uint8_t z_seed[32], uint64_t z_base,
+                                      const uint8_t* d_z, uint8_t check8[32]);
+int64_t edc_batch_submit_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* k,
+                                   const uint8_t z_seed[32], uint64_t z_base, int want_check8);
+int64_t edc_batch_submit_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                          const uint8_t* d_k, const uint8_t z_seed[32], uint64_t z_base,
+                                          const uint8_t* d_z, int want_check8);
+int edc_batch_verify_prehashed_fallback(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
+                                        const uint8_t* k, const uint8_t z_seed[32], uint8_t* verdicts,
+                                        int* n_invalid, uint8_t check8[32]);
+int edc_batch_verify_prehashed_fallback_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
+                                               const uint8_t* d_k, const uint8_t z_seed[32], uint8_t* verdicts,
+                                               int* n_invalid, uint8_t check8[32]);
+
+/*
  * batch::Item::verify_single (reference src/batch.rs:104-107): as edc_verify_each but with the
  * queue-time challenge k (n*32 bytes, canonical scalars) instead of the message.
  */
@@ -340,11 +379,15 @@ int edc_multi_batch_verify(edc_multi* m, size_t n, const uint8_t* vk, const uint
  * GPUs (reference src/batch.rs:149-217, one Verifier::verify per block): edc_multi_submit splits
  * the batch into contiguous shards, enqueues each on its device's next in-flight slot (host
  * inputs copied on that slot's stream, as edc_batch_submit) and returns a ticket >= 0 without
- * waiting. Each shard's 128-byte partial point (with its bad flag) is copied device to device to
- * the first device (peer copy over xGMI), where a combine on its own stream sums the partials
- * (x8, identity) as soon as the last shard lands. edc_multi_wait blocks for the ticket and
- * returns EDC_OK / EDC_INVALID_SIGNATURE / <0 with optional check8 (needs want_check8). Up to 16
- * batches in flight; tickets are waited in submission order; host buffers are borrowed until the
+ * waiting. Each shard's 128-byte partial point (with its bad flag) reaches the first device, where
+ * a combine on its own stream sums the partials (x8, identity) as soon as the last shard lands:
+ * by a peer store over xGMI when peer access from the shard's device to the first device could be
+ * enabled at edc_create_multi, otherwise through the shard slot's pinned host mirror (a 256-byte
+ * host-to-device copy on the combine stream); edc_create_multi fails (NULL) if enabling a
+ * possible peer access fails. edc_multi_wait blocks for the ticket and returns EDC_OK /
+ * EDC_INVALID_SIGNATURE / <0 with optional check8 (needs want_check8). Up to R batches in flight,
+ * R = 16 / (contexts sharing the busiest listed GPU), e.g. 16 for distinct devices, 8 for [0, 0];
+ * tickets are waited in submission order; host buffers are borrowed until the
  * wait. edc_multi_submit_device takes per-device slices already resident in each device's HBM:
  * n[g] items at d_vk[g], d_sig[g], d_msg[g], d_msg_off[g] form shard g, with global queue indices
  * (for z) starting at n[0] + ... + n[g-1]. Verdicts and check8 equal edc_batch_verify of the
@@ -356,6 +399,16 @@ int64_t edc_multi_submit_device(edc_multi* m, const size_t* n, const uint8_t* co
                                 const uint8_t* const* d_sig, const uint8_t* const* d_msg,
                                 const uint64_t* const* d_msg_off, const uint8_t z_seed[32], int want_check8);
 int edc_multi_wait(edc_multi* m, int64_t ticket, uint8_t check8[32]);
+/*
+ * How shard i's result block reaches the first device: 0 = same GPU (local copy), 1 = peer store
+ * over xGMI (peer access enabled), 2 = staged through pinned host memory. <0 for a bad index.
+ * Test knob: edc_multi_debug_force_staged(m, 1) routes every shard through host memory (the
+ * fallback a device pair without peer access takes); 0 restores the routes edc_create_multi found.
+ * Refused while batches are in flight. Status: distinct-device lists have not run on hardware in
+ * this repository's tests (the pool's boxes hold one GPU); the staged and local routes have.
+ */
+int edc_multi_route(const edc_multi* m, int i);
+int edc_multi_debug_force_staged(edc_multi* m, int on);
 /*
  * edc_multi_batch_verify and, on failure, the grouped fallback on every shard whose own partial
  * fails (edc_batch_verify_fallback_device semantics): verdicts (host, n bytes) = Item::verify_single

@@ -87,6 +87,48 @@ def test_multi_submit_fixture(multi, b):
             assert c8.hex() == b["expect_check8"]
 
 
+def test_multi_routes_and_ring(multi, edc):
+    """Every shard of a device list that repeats GPU 0 is routed locally; the multi ticket ring is
+    the shard contexts' share of the GPU's 16 slots (16 / contexts): that many batches can be in
+    flight, one more is refused cleanly (no shard slot is left half-submitted), and all verify."""
+    G = len(multi.devices)
+    assert [multi.route(i) for i in range(G)] == [0] * G
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == "batch_verify_one_bad"][0]
+    it = _items(b)
+    vks, sigs, msgs = [v for v, _, _ in it], [s for _, s, _ in it], [m for _, _, m in it]
+    zs = bytes.fromhex(b["z_seed"])
+    ring = 16 // G
+    ts = [multi.batch_submit(vks, sigs, msgs, zs, want_check8=True) for _ in range(ring)]
+    with pytest.raises(edc.EngineError, match="in flight"):
+        multi.batch_submit(vks, sigs, msgs, zs)
+    for t in ts:
+        code, c8 = multi.batch_wait(t, want_check8=True)
+        assert code == 1 and c8.hex() == b["expect_check8"]
+
+
+@pytest.mark.parametrize("b", golden("batches.json")["batches"], ids=lambda b: b["name"])
+def test_multi_submit_staged_route(multi, b):
+    """The route a shard takes when its device has no peer access to the first device (forced):
+    each shard's result block goes through its slot's pinned host mirror and a host-to-device copy
+    on the combine stream. Every golden batch, twice in flight: the fixture's verdict and [8]*check."""
+    multi.force_staged(True)
+    try:
+        assert all(multi.route(i) == 2 for i in range(len(multi.devices)))
+        it = _items(b)
+        vks, sigs, msgs = [v for v, _, _ in it], [s for _, s, _ in it], [m for _, _, m in it]
+        zs = bytes.fromhex(b["z_seed"])
+        t1 = multi.batch_submit(vks, sigs, msgs, zs, want_check8=True)
+        t2 = multi.batch_submit(vks, sigs, msgs, zs, want_check8=True)
+        for t in (t1, t2):
+            code, c8 = multi.batch_wait(t, want_check8=True)
+            assert code == b["expect_code"]
+            if b["expect_check8"] is not None:
+                assert c8.hex() == b["expect_check8"]
+    finally:
+        multi.force_staged(False)
+    assert multi.route(0) == 0
+
+
 def test_multi_submit_device_config3(multi, engine):
     """Device-resident pipelined form (edc_multi_submit_device) on configs[3] at 2^20: per-device
     slices of one batch (the ZIP215 corpus + one bad signature among 2^20 votes) -> Err, and the

@@ -48,6 +48,23 @@ def test_c_oracle_random_vs_python(oracle):
         assert oracle_c.batch_verify(items, zs) == oracle.batch_verify_seeded(items, zs)
 
 
+@pytest.mark.parametrize("name", ["two_bad_of_300", "repeated_keys_varlen", "undecodable_R", "c1_1024_distinct"])
+def test_c_oracle_parallel_ranges(name):
+    """The full-size checker (oracle_c.batch_verify_parallel: contiguous ranges at global z indices
+    on host threads, partials summed) equals the fixture for any range count."""
+    b = [x for x in golden("batches.json")["batches"] if x["name"] == name][0]
+    it = _items(b)
+    offs = [0]
+    for _, _, m in it:
+        offs.append(offs[-1] + len(m))
+    for parts in (1, 3, 8):
+        code, c8, _ = oracle_c.batch_verify_parallel(b"".join(v for v, _, _ in it), b"".join(s for _, s, _ in it),
+                                                     b"".join(m for _, _, m in it), offs, bytes.fromhex(b["z_seed"]),
+                                                     parts=parts)
+        assert code == b["expect_code"]
+        assert (c8.hex() if c8 else None) == b["expect_check8"]
+
+
 def test_c_oracle_shard_partials_combine():
     b = [x for x in golden("batches.json")["batches"] if x["name"] == "mixed_corpus_one_bad"][0]
     it = _items(b)

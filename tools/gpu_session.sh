@@ -1,0 +1,95 @@
+#!/bin/bash
+# GPU-box session runner (replaces the per-session gpu_r03*.sh scripts). Runs the named steps in
+# order, each under its own time limit, logs to gpurun_out/<tag>_<step>.log, and stops at the first
+# failure (a GPU fault, abort or time limit ends the call: nothing else touches the GPU after it).
+#
+#   tools/gpu_session.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   tests            every -m gpu test            tests=<pytest args>  a subset, e.g. tests=tests/test_gpu_prehashed.py
+#   smoke            __graft_entry__.smoke()
+#   driver           the driver's bench command (--gpus 1 --steps 20 --warmup 5, with the CPU baseline)
+#   c3 | c2 | c5     40-step benches of configs[2] / configs[1] / configs[4] (no CPU baseline)
+#   n17 | n18 | n19  2^17 / 2^18 / 2^19 shards of the vote batch (strong-scaling per-GPU rates)
+#   fallback         tools/fallback_bench.py (configs[3])    host  tools/host_bench.py
+#   small            tools/smallbatch_bench.py               multi tools/multi_bench.py
+#   prof             rocprofv3 kernel-trace stats of the bench, one batch at a time and pipelined
+#   rccl1            forced single-rank RCCL loop (process group + per-batch all-gather)
+#   gloo2            two ranks sharing the GPU over gloo, weak and strong
+#   ab=<v1,v2,..>    alternating A/B of variant builds csrc/libedc_<v>.so ("base" = libedc.so) on
+#                    AB_CONFIGS (default "c3 n17 c2 c5"), AB_REPS rounds (default 2)
+#   bench=<args>     one bench.py run with these arguments (commas for spaces)
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+tag=$1; shift
+D=ed25519-consensus_amd/csrc
+log() { echo "gpurun_out/${tag}_$1.log"; }
+
+run() {   # run <name> <timeout> <cmd...>: stop the session on failure
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$(log "$name")" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(tail -1 "$(log "$name")" | cut -c1-400)"
+  if [ $rc -ne 0 ]; then tail -15 "$(log "$name")"; exit $rc; fi
+}
+
+summ() {  # one line per bench log: value, ms/step, decode roofline fraction
+  python3 - "$1" "$2" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r = d.get("roofline", {})
+print(f"{sys.argv[2]:>14} {d['value']:.4e} sigs/s {d['ms_per_step']:.3f} ms/step frac {r.get('frac')} "
+      f"pipe {r.get('pipeline', {}).get('frac')} lat {d.get('batch_latency_ms')} "
+      + " ".join(f"{k[:8]}={v:.3f}" for k, v in d.get("phases_ms", {}).items()))
+EOF
+}
+
+bench_step() {   # bench_step <name> <args...>
+  local name=$1; shift
+  run "$name" 400 python3 -u bench.py "$@"
+  summ "$(log "$name")" "$name" | tee -a "gpurun_out/${tag}_summary.log"
+}
+
+for step in "$@"; do
+  case "$step" in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -s ;;
+    tests=*) run tests 900 python -u -m pytest ${step#tests=} -m gpu -x -v --timeout 300 --timeout-method thread -s ;;
+    smoke) run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    driver) bench_step driver --gpus 1 --steps 20 --warmup 5 ;;
+    c3) bench_step c3 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    c2) bench_step c2 --config c2 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    c5) bench_step c5 --config c5 --steps 12 --warmup 3 --no-cpu-baseline ;;
+    n17) bench_step n17 --n 131072 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    n18) bench_step n18 --n 262144 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    n19) bench_step n19 --n 524288 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    bench=*) bench_step bench ${step#bench=} ;;
+    fallback) run fallback 300 python3 -u tools/fallback_bench.py ;;
+    host) run host 300 python3 -u tools/host_bench.py ;;
+    small) run small 300 python3 -u tools/smallbatch_bench.py ;;
+    multi) run multi 300 python3 -u tools/multi_bench.py ;;
+    prof)
+      run prof1 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline
+      run profp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profp -o k -- python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    rccl1) run rccl1 300 env EDC_FORCE_DIST=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
+    gloo2)
+      run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
+      run gloo2_strong 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --scaling strong --steps 20 --warmup 3 --no-cpu-baseline ;;
+    ab=*)
+      IFS=, read -ra libs <<< "${step#ab=}"
+      for rep in $(seq 1 "${AB_REPS:-2}"); do
+        for v in "${libs[@]}"; do
+          lib=$D/libedc_$v.so; [ "$v" = base ] && lib=$D/libedc.so
+          for c in ${AB_CONFIGS:-c3 n17 c2 c5}; do
+            case $c in
+              c3) a="--steps 40";; c2) a="--config c2 --steps 40";; c5) a="--config c5 --steps 12";;
+              n17) a="--n 131072 --steps 40";; driver) a="--steps 20";; *) a="$c";;
+            esac
+            run ab 300 python3 -u bench.py $a --warmup 5 --no-cpu-baseline --profile-steps 1 --lib "$PWD/$lib"
+            summ "$(log ab)" "$c-$v" | tee -a "gpurun_out/${tag}_ab.log"
+          done
+        done
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
