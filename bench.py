@@ -198,6 +198,9 @@ def main():
     ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
     ap.add_argument("--msm-parts", type=int, default=0, help="MSM parts per batch (0 = chosen from the batch size)")
     ap.add_argument("--bin-entries", type=int, default=0, help="target MSM entries per bin (0 = chosen from the batch size)")
+    ap.add_argument("--prehashed", action="store_true",
+                    help="time edc_batch_submit_prehashed_device: items carry their queue-time k (the reference's "
+                         "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -253,13 +256,26 @@ def main():
     lib = eng.lib
     check8 = ctypes.create_string_buffer(32)
 
+    d_k = None
+    if args.prehashed:     # Item::from's k, computed once before timing (src/batch.rs:82-94)
+        o = (ctypes.c_uint64 * (n + 1)).from_buffer_copy((off - off[0]).cpu().numpy().astype("uint64").tobytes())
+        kb = ctypes.create_string_buffer(32 * max(n, 1))
+        eng._check(lib.edc_challenge(eng.ctx, n, vk[:32 * n].cpu().numpy().tobytes(), sig[:64 * n].cpu().numpy().tobytes(),
+                                     msg.cpu().numpy().tobytes(), o, kb))
+        d_k = torch.frombuffer(bytearray(kb.raw), dtype=torch.uint8).to(dev)
+        torch.cuda.synchronize()
+
     pending = []
     combine = (lambda p, b: eng.combine_partials(p, b, want_check8=False))
     allgather = sharded.torch_allgather_fn(dist, dev if backend != "gloo" else torch.device("cpu")) if dist else None
 
     def submit():
-        t = lib.edc_batch_submit_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
-                                        zseed, base, None, 0)
+        if d_k is not None:
+            t = lib.edc_batch_submit_prehashed_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), d_k.data_ptr(), zseed,
+                                                      base, None, 0)
+        else:
+            t = lib.edc_batch_submit_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(), off.data_ptr(),
+                                            zseed, base, None, 0)
         if t < 0:
             eng._check(t)
         pending.append(t)
@@ -409,6 +425,7 @@ def main():
             "config": {"workload": c_desc,
                        "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
                        "inflight": args.inflight, "keycache": bool(args.keycache and args.keys > 0),
+                       "prehashed": bool(args.prehashed),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

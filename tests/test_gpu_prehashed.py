@@ -179,12 +179,14 @@ def test_config2_prehashed_equals_message_path(engine):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("kind", ["bad_R", "bad_s", "bad_A"])
+@pytest.mark.parametrize("kind", ["bad_R", "bad_s", "bad_A", "wrong_msg", "valid"])
 def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
     """Slot 0 (synchronous calls) decodes on a second stream beside SHA-512 / coefficients /
-    binning; the pipelined slots run everything on one stream. A batch that fails in the decode
-    (R or key not on the curve) or in the s check gives the same bad flag and the same partial
-    point on both, and slot 0's grouped fallback agrees with the per-item kernel."""
+    binning; the pipelined slots run everything on one stream. On both: the same verdict and bad
+    flag; for batches whose points all decode (s >= l, a wrong message, valid) the same partial
+    point ([8]*P compared, partials being projective); slot 0's grouped fallback agrees with the
+    per-item kernel. (An undecodable R or key leaves an off-curve point in the MSM: its sum then
+    depends on the addition order and is not compared; the batch is rejected by its bad flag.)"""
     torch = pytest.importorskip("torch")
     import random
     dev = torch.device("cuda:0")
@@ -201,8 +203,10 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
         elif kind == "bad_s":
             s = int.from_bytes(sigs[p][32:], "little") + L_ORDER
             sigs[p] = sigs[p][:32] + s.to_bytes(32, "little")
-        else:
+        elif kind == "bad_A":
             vks[p] = bytes.fromhex(dec_bad[0]["enc"])
+        elif kind == "wrong_msg":
+            msgs[p] = msgs[p][:-1] + bytes([msgs[p][-1] ^ 1])
     offs = [0]
     for m in msgs:
         offs.append(offs[-1] + len(m))
@@ -215,7 +219,9 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
     p0, f0 = ctypes.create_string_buffer(128), ctypes.c_int(0)
     assert lib.edc_batch_partial_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
                                         d_off.data_ptr(), zseed, 0, None, p0, ctypes.byref(f0)) == 0
-    assert f0.value == 1
+    bad_flag = 1 if kind in ("bad_R", "bad_s", "bad_A") else 0
+    verdict = 0 if kind == "valid" else 1
+    assert f0.value == bad_flag
     assert lib.edc_set_slots(engine.ctx, 16) == 0            # tickets 0, 1, 2, 3 -> slots 0, 1, 2, 3
     tickets = []
     for _ in range(4):          # four batches in flight at once: slot 0 (two streams) and slots 1-3 (one)
@@ -226,15 +232,20 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
     assert tickets == [0, 1, 2, 3]
     # partials are projective (X:Y:Z:T in the order the MSM summed): compare [8]*P compressed
     ref = engine.combine_partials([p0.raw], False)
-    assert ref[1] != bytes(32)
+    if kind in ("valid", "bad_s"):      # s + l: the same scalar mod l, rejected only by the bad flag
+        assert ref == (0, IDENTITY)
+    elif kind == "wrong_msg":
+        assert ref[0] == 1 and ref[1] != IDENTITY
     for t in tickets:
         p1, f1 = ctypes.create_string_buffer(128), ctypes.c_int(0)
-        assert lib.edc_batch_wait(engine.ctx, t, None, p1, ctypes.byref(f1)) == 1
-        assert f1.value == 1 and engine.combine_partials([p1.raw], False) == ref
+        assert lib.edc_batch_wait(engine.ctx, t, None, p1, ctypes.byref(f1)) == verdict
+        assert f1.value == bad_flag
+        if not bad_flag or kind == "bad_s":
+            assert engine.combine_partials([p1.raw], False) == ref
     v = ctypes.create_string_buffer(n)
     cnt = ctypes.c_int(0)
     assert lib.edc_batch_verify_fallback_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
-                                                d_off.data_ptr(), zseed, v, ctypes.byref(cnt), None) == 1
+                                                d_off.data_ptr(), zseed, v, ctypes.byref(cnt), None) == verdict
     d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
     assert lib.edc_verify_each_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), d_msg.data_ptr(),
                                       d_off.data_ptr(), d_v.data_ptr()) == 0

@@ -19,6 +19,7 @@
 #   ab=<v1,v2,..>    alternating A/B of variant builds csrc/libedc_<v>.so ("base" = libedc.so) on
 #                    AB_CONFIGS (default "c3 n17 c2 c5"), AB_REPS rounds (default 2)
 #   bench=<args>     one bench.py run with these arguments (commas for spaces)
+#   pre              configs[2] with prehashed items (edc_batch_submit_prehashed_device)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -63,7 +64,8 @@ for step in "$@"; do
     n17) bench_step n17 --n 131072 --steps 40 --warmup 5 --no-cpu-baseline ;;
     n18) bench_step n18 --n 262144 --steps 40 --warmup 5 --no-cpu-baseline ;;
     n19) bench_step n19 --n 524288 --steps 40 --warmup 5 --no-cpu-baseline ;;
-    bench=*) bench_step bench ${step#bench=} ;;
+    bench=*) a=${step#bench=}; bench_step bench ${a//,/ } ;;
+    pre) bench_step pre --prehashed --steps 40 --warmup 5 --no-cpu-baseline ;;
     fallback) run fallback 300 python3 -u tools/fallback_bench.py ;;
     host) run host 300 python3 -u tools/host_bench.py ;;
     small) run small 300 python3 -u tools/smallbatch_bench.py ;;

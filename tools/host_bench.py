@@ -86,6 +86,54 @@ def main():
         el = time.perf_counter() - t0
         out[kind + "_streamed"] = {"sigs_per_s": round(n * args.steps / el, 1),
                                    "ms_per_batch": round(el / args.steps * 1e3, 3), "inflight": args.inflight}
+    # prehashed items (the reference's Item {vk_bytes, sig, k}, src/batch.rs:76-80): k computed
+    # once before timing (at Item::from), then 128 B per item cross PCIe and SHA-512 is skipped
+    ho_all = off.cpu()
+    offs = (ctypes.c_uint64 * (n + 1)).from_buffer_copy(ho_all.numpy().astype("uint64").tobytes())
+    kbuf = ctypes.create_string_buffer(32 * n)
+    hv0, hs0 = vk[:32 * n].cpu(), sig[:64 * n].cpu()
+    eng._check(lib.edc_challenge(eng.ctx, n, hv0.numpy().tobytes(), hs0.numpy().tobytes(), msg.cpu().numpy().tobytes(),
+                                 offs, kbuf))
+    k_host = torch.frombuffer(bytearray(kbuf.raw), dtype=torch.uint8)
+    for kind in ("pageable", "pinned"):
+        pin = kind == "pinned"
+        hv, hs, hk = (t.pin_memory() if pin else t for t in (hv0, hs0, k_host))
+        ptr = lambda t: ctypes.cast(ctypes.c_void_p(t.data_ptr()), ctypes.c_char_p)
+
+        def step_pre():
+            rc = lib.edc_batch_verify_prehashed(eng.ctx, n, ptr(hv), ptr(hs), ptr(hk), zseed, None, None)
+            assert rc == 0, f"valid prehashed batch rejected: {rc} {eng.lib.edc_last_error(eng.ctx)}"
+
+        for _ in range(args.warmup):
+            step_pre()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_pre()
+        el = time.perf_counter() - t0
+        nbytes = hv.numel() + hs.numel() + hk.numel()
+        out[kind + "_prehashed"] = {"sigs_per_s": round(n * args.steps / el, 1),
+                                    "ms_per_batch": round(el / args.steps * 1e3, 3), "bytes_per_sig": round(nbytes / n, 1)}
+        pending = []
+
+        def stream_pre(k):
+            for _ in range(k):
+                if len(pending) >= args.inflight:
+                    rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
+                    assert rc == 0, rc
+                t = lib.edc_batch_submit_prehashed(eng.ctx, n, ptr(hv), ptr(hs), ptr(hk), zseed, 0, 0)
+                assert t >= 0, eng.lib.edc_last_error(eng.ctx)
+                pending.append(t)
+            while pending:
+                rc = lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None)
+                assert rc == 0, rc
+
+        stream_pre(args.warmup)
+        t0 = time.perf_counter()
+        stream_pre(args.steps)
+        el = time.perf_counter() - t0
+        out[kind + "_streamed_prehashed"] = {"sigs_per_s": round(n * args.steps / el, 1),
+                                             "ms_per_batch": round(el / args.steps * 1e3, 3),
+                                             "bytes_per_sig": round(nbytes / n, 1), "inflight": args.inflight}
     # key-indexed streaming (edc_batch_submit_indexed): the validator set registered once, votes
     # carry a 4-byte validator index instead of the 32-byte key
     if keys > 0:
