@@ -111,6 +111,20 @@ EDC_HD fe fe_sub(const fe& a, const fe& b) {
 
 EDC_HD fe fe_neg(const fe& a) { return fe_sub(fe_zero(), a); }
 
+// Lazy subtraction, no carry pass: a limbs < 2^30 + 2^20 (reduced, or a lazy sum of two reduced),
+// b limbs <= K_i -> limbs < 2^31.61. Such an element is a valid fe_mul operand ONLY against a
+// REDUCED partner (limbs < 2^29 + 2^19): a column then holds at most 9 products
+// < 2^31.61 * 2^29.002 = 2^60.61, i.e. < 2^63.78 with the fold terms, inside the 64-bit
+// accumulator (fe_mul's symmetric bound, 2^30.41 per operand, is the other admissible case).
+// Point formulas use it on one side of every product whose other side is carried.
+EDC_HD fe fe_sub_lazy(const fe& a, const fe& b) {
+  fe t;
+  t.v[0] = a.v[0] + EDC_SUB_K0 - b.v[0];
+  for (int i = 1; i < 8; ++i) t.v[i] = a.v[i] + EDC_SUB_K1 - b.v[i];
+  t.v[8] = a.v[8] + EDC_SUB_K8 - b.v[8];
+  return t;
+}
+
 // Top-column fold shared by mul and sqr: acc = the carry out of column 8 (< 2^35), i.e. the
 // value acc * 2^261 == acc * 1216 still to be added at limb 0.
 EDC_HD fe fe_fold_top(fe r, uint64_t top) {
@@ -125,7 +139,8 @@ EDC_HD fe fe_fold_top(fe r, uint64_t top) {
 // mod p) are summed first; low column k then starts from the carry out of column k-1, so the
 // carry rides in a mad addend instead of a separate 64-bit add, and it absorbs the fold terms
 // lo32(col k+9) * 1216 and hi32(col k+8) * 2^32 * 1216 = hi * 9728 as two more products.
-// Column bound: 9 products < 2^60.82 (inputs < 2^30.41) + fold < 2^45.3 + carry < 2^35 < 2^64.
+// Column bound: 9 products < 2^60.82 (inputs < 2^30.41) + fold < 2^45.3 + carry < 2^35 < 2^64;
+// or one input reduced (< 2^29.002) and the other < 2^31.83 (fe_sub_lazy outputs: < 2^31.61).
 EDC_HD fe fe_mul(const fe& a, const fe& b) {
   uint64_t h[8];
 #pragma unroll

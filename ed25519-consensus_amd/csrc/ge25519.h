@@ -97,16 +97,21 @@ EDC_HD ge_p3 ge_neg(const ge_p3& P) {
 #define EDC_SCHED_FENCE() ((void)0)
 #endif
 
+// Carry passes in the addition formulas. E, F, G, H each meet two others in X3 = EF, Y3 = GH,
+// T3 = EH, Z3 = FG (a 4-cycle), so carrying F and H alone puts a reduced operand in every
+// product; E = B - A and G = D +- C stay lazy (fe_sub_lazy bound), as does Y1 - X1 against the
+// reduced record half and D = 2 Z1. Two carry passes per addition instead of four. Inputs: P's
+// coordinates and the record's fields reduced (every producer ends in fe_mul / fe_sub / fe_add_c).
 // P + Q, Q affine Niels: 7M
 EDC_HD ge_p3 ge_madd(const ge_p3& P, const ge_niels& q) {
-  fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  fe A = fe_mul(fe_sub_lazy(P.Y, P.X), q.ymx);
   EDC_SCHED_FENCE();
   fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
   EDC_SCHED_FENCE();
   fe C = fe_mul(P.T, q.xy2d);
   EDC_SCHED_FENCE();
-  fe D = fe_add_c(P.Z, P.Z);
-  fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  fe D = fe_add(P.Z, P.Z);
+  fe E = fe_sub_lazy(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add_c(B, A);
   ge_p3 r;
   r.X = fe_mul(E, F);
   EDC_SCHED_FENCE();
@@ -120,15 +125,15 @@ EDC_HD ge_p3 ge_madd(const ge_p3& P, const ge_niels& q) {
 
 // P + Q, Q projective Niels: 8M
 EDC_HD ge_p3 ge_add_cached(const ge_p3& P, const ge_cached& q) {
-  fe A = fe_mul(fe_sub(P.Y, P.X), q.ymx);
+  fe A = fe_mul(fe_sub_lazy(P.Y, P.X), q.ymx);
   EDC_SCHED_FENCE();
   fe B = fe_mul(fe_add(P.Y, P.X), q.ypx);
   EDC_SCHED_FENCE();
   fe C = fe_mul(P.T, q.T2d);
   EDC_SCHED_FENCE();
   fe ZZ = fe_mul(P.Z, q.Z);
-  fe D = fe_add_c(ZZ, ZZ);
-  fe E = fe_sub(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add(B, A);
+  fe D = fe_add(ZZ, ZZ);
+  fe E = fe_sub_lazy(B, A), F = fe_sub(D, C), G = fe_add(D, C), H = fe_add_c(B, A);
   ge_p3 r;
   r.X = fe_mul(E, F);
   EDC_SCHED_FENCE();
@@ -145,16 +150,17 @@ EDC_HD ge_p3 ge_add_cached(const ge_p3& P, const ge_cached& q) {
 // 36 selects instead of ge_niels_neg's swap, negation and select of the whole record.
 EDC_HD ge_p3 ge_madd_sgn(const ge_p3& P, const ge_niels& q, bool neg) {
   const fe ym = fe_select(q.ymx, q.ypx, neg), yp = fe_select(q.ypx, q.ymx, neg);
-  fe A = fe_mul(fe_sub(P.Y, P.X), ym);
+  fe A = fe_mul(fe_sub_lazy(P.Y, P.X), ym);
   EDC_SCHED_FENCE();
   fe B = fe_mul(fe_add(P.Y, P.X), yp);
   EDC_SCHED_FENCE();
   fe C = fe_mul(P.T, q.xy2d);
   EDC_SCHED_FENCE();
-  fe D = fe_add_c(P.Z, P.Z);
-  fe E = fe_sub(B, A), H = fe_add(B, A);
-  const fe dmc = fe_sub(D, C), dpc = fe_add(D, C);
-  fe F = fe_select(dmc, dpc, neg), G = fe_select(dpc, dmc, neg);
+  fe D = fe_add(P.Z, P.Z);
+  fe E = fe_sub_lazy(B, A), H = fe_add_c(B, A);
+  const fe dmc = fe_sub_lazy(D, C), dpc = fe_add(D, C);
+  // F (carried) is D - C, or D + C for -Q; G keeps the other one lazy
+  fe F = fe_carry(fe_select(dmc, dpc, neg)), G = fe_select(dpc, dmc, neg);
   ge_p3 r;
   r.X = fe_mul(E, F);
   EDC_SCHED_FENCE();
@@ -183,7 +189,7 @@ EDC_HD ge_p3 ge_dbl(const ge_p3& P, bool with_t = true) {
   fe Yc = fe_add(YY, XX);
   fe Zc = fe_sub(YY, XX);
   fe Xc = fe_sub(XpY2, Yc);
-  fe Tc = fe_sub(ZZ2, Zc);
+  fe Tc = fe_sub_lazy(ZZ2, Zc);     // lazy: meets only Xc and Zc (both carried)
   ge_p3 r;
   r.X = fe_mul(Xc, Tc);
   EDC_SCHED_FENCE();

@@ -41,7 +41,16 @@ static const uint64_t SHA512_K[80] = {
 // register pairs; a 32-bit-halves formulation costs v_mov shuffles to rebuild the pairs).
 EDC_HD uint32_t lo32(uint64_t x) { return (uint32_t)x; }
 EDC_HD uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+// On the device the pair is built as a bit cast of a 2 x u32 vector: the halves land in one
+// register pair and the 64-bit adds take it whole. Written as (hi << 32) | lo, LLVM instead
+// re-associated every sum into separate zero-extended lo / hi contributions: per round three more
+// v_lshl_add_u64 and four v_mov_b32 (34 instead of 27 VALU instructions per round).
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t edc_u32x2 __attribute__((ext_vector_type(2)));
+EDC_HD uint64_t mk64(uint32_t lo, uint32_t hi) { return __builtin_bit_cast(uint64_t, edc_u32x2{lo, hi}); }
+#else
 EDC_HD uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+#endif
 // funnel shift right of hi:lo by n (0 < n < 32)
 EDC_HD uint32_t fshr32(uint32_t hi, uint32_t lo, int n) {
 #if defined(__HIP_DEVICE_COMPILE__)

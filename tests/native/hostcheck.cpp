@@ -101,6 +101,28 @@ int hc_point_ops(const uint8_t* a, const uint8_t* b, uint8_t* sum, uint8_t* dbl,
   return 1;
 }
 
+// out = compress(a + b) or compress(a - b) through ge_madd_sgn (the accumulation's signed
+// mixed addition), after `pre` doublings of a (so the accumulator is a projective point)
+int hc_point_madd_sgn(const uint8_t* a, const uint8_t* b, int neg, int pre, uint8_t* out) {
+  uint32_t wa[8], wb[8], w[8];
+  bytes_to_words(a, wa);
+  bytes_to_words(b, wb);
+  ge_p3 P, Q;
+  if (!ge_decompress(wa, P) || !ge_decompress(wb, Q)) return 0;
+  for (int i = 0; i < pre; ++i) P = ge_dbl(P);
+  ge_compress(ge_madd_sgn(P, ge_to_niels_affine(Q), neg != 0), w);
+  words_to_bytes(w, out);
+  return 1;
+}
+
+// fe_sub_lazy(a, b) limbs (a, b raw limbs)
+void hc_fe_sub_lazy(const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  fe x, y;
+  for (int i = 0; i < 9; ++i) { x.v[i] = a[i]; y.v[i] = b[i]; }
+  fe r = fe_sub_lazy(x, y);
+  for (int i = 0; i < 9; ++i) out[i] = r.v[i];
+}
+
 void hc_sha512(const uint8_t* head0, const uint8_t* head1, const uint8_t* msg, uint64_t mlen,
                uint8_t* out) {
   sha_src s{head0, head1, msg, mlen};

@@ -86,6 +86,52 @@ def test_mul_at_input_bound(hc, oracle):
             assert max(lim) < (1 << 29) + (1 << 19), (op, list(lim))
 
 
+def test_mul_lazy_sub_operand_at_bound(hc, oracle):
+    """The asymmetric fe_mul bound the point formulas rely on (fe25519.h fe_sub_lazy): one
+    operand a lazy difference at its largest (D = 2Z at its lazy maximum minus 0, limbs up to
+    2^31.61), the other reduced at its largest (limbs 2^29 + 2^19 - 1): exact mod p, reduced out."""
+    P = oracle.P
+    rnd = random.Random(31)
+    LimbsT = ctypes.c_uint32 * 9
+    red = (1 << 29) + (1 << 19) - 1
+    dmax = 2 * red
+    out = ctypes.create_string_buffer(32)
+    lim, lz = LimbsT(), LimbsT()
+    cases = [([dmax] * 9, [0] * 9), ([dmax] * 9, [red] * 9)]
+    cases += [([rnd.randrange(dmax + 1) for _ in range(9)], [rnd.randrange(red + 1) for _ in range(9)])
+              for _ in range(200)]
+    val = lambda x: sum(v << (29 * k) for k, v in enumerate(x))
+    for a, b in cases:
+        hc.hc_fe_sub_lazy(LimbsT(*a), LimbsT(*b), lz)
+        assert val(list(lz)) % P == (val(a) - val(b)) % P
+        assert max(lz) < 2**31.61
+        for partner in ([red] * 9, [rnd.randrange(red + 1) for _ in range(9)]):
+            for x, y in ((list(lz), partner), (partner, list(lz))):
+                hc.hc_fe_limbs(0, LimbsT(*x), LimbsT(*y), out, lim)
+                assert int.from_bytes(out.raw, "little") == val(x) * val(y) % P
+                assert max(lim) < (1 << 29) + (1 << 19)
+
+
+def test_signed_mixed_addition(hc, oracle):
+    """ge_madd_sgn (the bucket accumulation's addition, lazy carries) for both signs, on affine and
+    projective accumulators, against the oracle."""
+    from conftest import golden
+    valid = [bytes.fromhex(c["enc"]) for c in golden("decode.json")["cases"] if c["ok"]]
+    out = ctypes.create_string_buffer(32)
+    rnd = random.Random(13)
+    for _ in range(80):
+        e1, e2 = rnd.choice(valid), rnd.choice(valid)
+        P1, P2 = oracle.decompress(e1), oracle.decompress(e2)
+        for pre in (0, 3):
+            A = P1
+            for _ in range(pre):
+                A = oracle.double(A)
+            for neg in (0, 1):
+                assert hc.hc_point_madd_sgn(e1, e2, neg, pre, out)
+                exp = oracle.add(A, oracle.neg(P2) if neg else P2)
+                assert out.raw == oracle.compress(exp)
+
+
 def test_decompress_and_point_ops(hc, oracle):
     from conftest import golden
     out = ctypes.create_string_buffer(64)

@@ -88,7 +88,7 @@ for step in "$@"; do
               n17) a="--n 131072 --steps 40";; driver) a="--steps 20";; *) a="$c";;
             esac
             run ab 300 python3 -u bench.py $a --warmup 5 --no-cpu-baseline --profile-steps 1 --lib "$PWD/$lib"
-            summ "$(log ab)" "$c-$v" | tee -a "gpurun_out/${tag}_ab.log"
+            summ "$(log ab)" "$c-$v" | tee -a "gpurun_out/${tag}_ab_summary.log"
           done
         done
       done ;;
