@@ -198,6 +198,9 @@ def main():
     ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
     ap.add_argument("--msm-parts", type=int, default=0, help="MSM parts per batch (0 = chosen from the batch size)")
     ap.add_argument("--bin-entries", type=int, default=0, help="target MSM entries per bin (0 = chosen from the batch size)")
+    ap.add_argument("--multi", type=int, default=1,
+                    help="verify this many consecutive batches of --n signatures per launch sequence "
+                         "(edc_batch_submit_multi_device; each keeps its own verdict and z range)")
     ap.add_argument("--prehashed", action="store_true",
                     help="time edc_batch_submit_prehashed_device: items carry their queue-time k (the reference's "
                          "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
@@ -241,15 +244,16 @@ def main():
     # per GPU the hardware scheduler time-slices them ("One hardware queue per slot")
     sharing = max(1, -(-world // max(1, torch.cuda.device_count()))) if backend == "gloo" else 1
     slots = max(1, 16 // sharing)
+    nmb = max(1, args.multi)                       # batches per launch sequence
     if args.inflight <= 0:
-        args.inflight = 6 if n >= (1 << 19) else 16
+        args.inflight = 6 if n * nmb >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)
     # the context rotates over exactly `inflight` slots, so only that many slot streams (hardware
     # queues) exist beside RCCL's own in a multi-rank run; a build with fewer slots keeps its count
     if eng.lib.edc_set_slots(eng.ctx, args.inflight) < 0 and sharing > 1:
         raise RuntimeError("cannot split the GPU's slots between the ranks sharing it")
     t_gen = time.perf_counter()
-    vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
+    vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n * nmb, args.keys, args.msg_len, base * nmb)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
     zseed = bytes([0x33]) * 32
@@ -258,10 +262,11 @@ def main():
 
     d_k = None
     if args.prehashed:     # Item::from's k, computed once before timing (src/batch.rs:82-94)
-        o = (ctypes.c_uint64 * (n + 1)).from_buffer_copy((off - off[0]).cpu().numpy().astype("uint64").tobytes())
-        kb = ctypes.create_string_buffer(32 * max(n, 1))
-        eng._check(lib.edc_challenge(eng.ctx, n, vk[:32 * n].cpu().numpy().tobytes(), sig[:64 * n].cpu().numpy().tobytes(),
-                                     msg.cpu().numpy().tobytes(), o, kb))
+        nt = n * nmb
+        o = (ctypes.c_uint64 * (nt + 1)).from_buffer_copy((off - off[0]).cpu().numpy().astype("uint64").tobytes())
+        kb = ctypes.create_string_buffer(32 * max(nt, 1))
+        eng._check(lib.edc_challenge(eng.ctx, nt, vk[:32 * nt].cpu().numpy().tobytes(),
+                                     sig[:64 * nt].cpu().numpy().tobytes(), msg.cpu().numpy().tobytes(), o, kb))
         d_k = torch.frombuffer(bytearray(kb.raw), dtype=torch.uint8).to(dev)
         torch.cuda.synchronize()
 
@@ -270,7 +275,11 @@ def main():
     allgather = sharded.torch_allgather_fn(dist, dev if backend != "gloo" else torch.device("cpu")) if dist else None
 
     def submit():
-        if d_k is not None:
+        if nmb > 1:
+            t = lib.edc_batch_submit_multi_device(eng.ctx, nmb, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                                  off.data_ptr(), d_k.data_ptr() if d_k is not None else None, zseed,
+                                                  base * nmb, 0)
+        elif d_k is not None:
             t = lib.edc_batch_submit_prehashed_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), d_k.data_ptr(), zseed,
                                                       base, None, 0)
         else:
@@ -282,6 +291,11 @@ def main():
 
     def wait_oldest():
         """Collect the oldest batch; returns a function that completes its verdict."""
+        if nmb > 1:
+            assert dist is None, "--multi runs on one process per node"
+            v = (ctypes.c_int * nmb)()
+            rc = eng._check(lib.edc_batch_wait_multi(eng.ctx, pending.pop(0), nmb, v, None, None, None))
+            return lambda: rc
         if dist is None:
             rc = eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None))
             return lambda: rc
@@ -375,7 +389,7 @@ def main():
     phases = {names[i]: round(acc[i], 4) for i in range(7)}
 
     if rank == 0:
-        total = n * world * args.steps          # strong scaling: n * world == --n
+        total = n * nmb * world * args.steps    # strong scaling: n * world == --n
         value = total / elapsed
         ms_per_step = elapsed / args.steps * 1e3
         dom_ms = phases["decompress_R"]
@@ -425,7 +439,7 @@ def main():
             "config": {"workload": c_desc,
                        "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
                        "inflight": args.inflight, "keycache": bool(args.keycache and args.keys > 0),
-                       "prehashed": bool(args.prehashed),
+                       "prehashed": bool(args.prehashed), "batches_per_launch": nmb,
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

@@ -49,6 +49,7 @@ ABI_SYMBOLS = [
     "edc_batch_verify_prehashed", "edc_batch_verify_prehashed_device", "edc_batch_submit_prehashed",
     "edc_batch_submit_prehashed_device", "edc_batch_verify_prehashed_fallback",
     "edc_batch_verify_prehashed_fallback_device", "edc_multi_route", "edc_multi_debug_force_staged",
+    "edc_batch_submit_multi_device", "edc_batch_wait_multi",
 ]
 
 
@@ -157,6 +158,12 @@ def load_library(path=None):
         lib.edc_multi_submit_device.argtypes = [c_vp, ctypes.POINTER(c_sz), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp),
                                                 ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_u8p, ctypes.c_int]
         lib.edc_multi_wait.argtypes = [c_vp, ctypes.c_int64, c_vp]
+        if hasattr(lib, "edc_batch_submit_multi_device"):
+            lib.edc_batch_submit_multi_device.restype = ctypes.c_int64
+            lib.edc_batch_submit_multi_device.argtypes = [c_vp, c_sz, c_sz, c_vp, c_vp, c_vp, c_vp, c_vp, c_u8p,
+                                                          ctypes.c_uint64, ctypes.c_int]
+            lib.edc_batch_wait_multi.argtypes = [c_vp, ctypes.c_int64, c_sz, ctypes.POINTER(ctypes.c_int), c_vp, c_vp,
+                                                 ctypes.POINTER(ctypes.c_int)]
         if hasattr(lib, "edc_multi_route"):
             lib.edc_multi_route.argtypes = [c_vp, ctypes.c_int]
             lib.edc_multi_debug_force_staged.argtypes = [c_vp, ctypes.c_int]
@@ -323,6 +330,28 @@ class Engine:
                 self._check(t)
             self._host_inflight[t] = bufs
         return t
+
+    def batch_submit_multi_device(self, nb, n_per, d_vk, d_sig, d_msg, d_off, z_seed, z_base=0, d_k=None,
+                                  want_check8=False):
+        """nb consecutive batches of n_per items in one launch sequence (edc_batch_submit_multi_device);
+        device pointers as ints. Returns a ticket for batch_wait_multi."""
+        with self._lock:
+            t = self.lib.edc_batch_submit_multi_device(self.ctx, nb, n_per, d_vk, d_sig, d_msg, d_off, d_k,
+                                                       bytes(z_seed), z_base, 1 if want_check8 else 0)
+        self._check(t)
+        return t
+
+    def batch_wait_multi(self, ticket, nb):
+        """(code, [verdict per batch], [check8 per batch], [partial per batch], [bad per batch])."""
+        v = (ctypes.c_int * nb)()
+        bad = (ctypes.c_int * nb)()
+        c8 = ctypes.create_string_buffer(32 * nb)
+        parts = ctypes.create_string_buffer(128 * nb)
+        with self._lock:
+            rc = self.lib.edc_batch_wait_multi(self.ctx, ticket, nb, v, c8, parts, bad)
+        self._check(rc)
+        return (rc, list(v), [c8.raw[32 * g:32 * g + 32] for g in range(nb)],
+                [parts.raw[128 * g:128 * g + 128] for g in range(nb)], list(bad))
 
     def batch_wait(self, ticket, want_check8=False):
         """Verdict of a submitted batch: (code, check8 or None); the ticket's host buffers are released."""

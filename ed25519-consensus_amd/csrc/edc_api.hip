@@ -44,6 +44,8 @@ constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
 #define EDC_DUAL_STREAM 2   // slot 0 (synchronous calls) decodes on a second stream; see init_slot
 #endif
 constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
+constexpr uint32_t kMultiMax = 16;            // batches per edc_batch_submit_multi_device launch
+constexpr uint32_t kMultiKeys = 4096;         // distinct keys with per-(batch, key) sums; more -> per signature
 
 }  // namespace
 
@@ -70,8 +72,15 @@ struct Slot {
   uint32_t* heads = nullptr;    // bins x 256 head partials of the segmented accumulation
   uint32_t* bucket_end = nullptr;   // bins x 256 bucket end positions of the sorted entries
   int* flags = nullptr;
-  uint8_t* d_out = nullptr;     // 256-byte result block
+  uint8_t* d_out = nullptr;     // 256-byte result block (kMultiMax of them for a multi-batch launch)
   uint8_t* h_out = nullptr;     // pinned mirror
+  // several batches in one launch (edc_batch_submit_multi_device): per-(batch, key) sums, listed
+  // key / B terms, per-batch bad flags; nmulti = batches of the pending launch (0: one batch)
+  unsigned long long* mb_acc = nullptr;
+  uint32_t *mb_xpt = nullptr, *mb_xrg = nullptr, *mb_xscal = nullptr;
+  uint8_t* mb_bad = nullptr;
+  size_t mb_cap_acc = 0, mb_cap_terms = 0;
+  uint32_t nmulti = 0;
   hipEvent_t ev[PH_N + 1] = {};
   // EDC_DUAL_STREAM builds: the decode runs on a second stream beside SHA-512 / coefficients /
   // binning (joined before the accumulation)
@@ -211,8 +220,8 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   if (s.st) return 0;
   CK(create_slot_stream(ctx->device, &s.st));
   CK(dalloc(&s.flags, FLAG_COUNT));
-  CK(dalloc(&s.d_out, 256));
-  CK(hipHostMalloc((void**)&s.h_out, 256));
+  CK(dalloc(&s.d_out, 256 * kMultiMax));
+  CK(hipHostMalloc((void**)&s.h_out, 256 * kMultiMax));
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
 #if EDC_DUAL_STREAM
   // 1: every slot; 2: slot 0 only (the synchronous calls' slot), so the pipelined slots keep one
@@ -610,6 +619,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
   s.kin = d_k ? d_k : s.k;
+  s.nmulti = 0;
   const uint32_t N = (uint32_t)n;
   const uint32_t T = (uint32_t)next_pow2(2 * (n < 128 ? 128 : n));
   if (T > s.cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
@@ -698,9 +708,152 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   return 0;
 }
 
+// ---- several batches in one launch sequence (edc_batch_submit_multi_device) ----
+// nb consecutive batches of n_per items each (a node verifying several blocks at once, or one
+// GPU's shards of consecutive blocks): every per-item kernel runs once over all nb * n_per items,
+// so small batches fill the GPU like one large batch, and the MSM is range-tagged (one range per
+// batch, the plan of an n_per batch in each) with one Horner, verdict, check8 and partial per
+// range. Batch b's z are drawn at z_base + b n_per + i: its results equal a separate
+// edc_batch_verify_device / edc_batch_partial_device of batch b at that z_base. The grouped
+// fallback's range machinery (k_coef range mode, listed key / B terms) with the key count left
+// on the device: per-(batch, key) sums sit at b * kstride + key and the term layout is resolved
+// from the key grouping by the binning kernels (MsmTerms::dyn).
+static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
+                         const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_k, const uint8_t* z_seed,
+                         uint64_t z_base, int want_compress) {
+  if (nb < 1 || nb > kMultiMax || n_per == 0 || n_per % COEF_CHUNK) {
+    ctx->err = "multi-batch: 1..16 batches of a multiple of 2048 items each";
+    return EDC_ERR_ARG;
+  }
+  const size_t N = (size_t)nb * n_per;
+  if (N >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
+  if (!aligned16(d_vk) || !aligned16(d_sig) || (d_k && !aligned16(d_k))) {
+    ctx->err = "device vk / sig / k arrays must be 16-byte aligned";
+    return EDC_ERR_ARG;
+  }
+  if (!d_k && (!d_msg || !d_off)) { ctx->err = "null msg"; return EDC_ERR_ARG; }
+  int rc = ensure_slot(ctx, s, N);
+  if (rc) return rc;
+  const bool per_sig = choose_per_sig(ctx, N);
+  const uint32_t kstride = (uint32_t)(N < kMultiKeys ? N : kMultiKeys);
+  MsmPlan P = batch_plan(ctx, n_per, per_sig, false);
+  P.nranges = nb;
+  P.sum_ranges = 0;
+  if (P.bins_per_range * nb > MSM_MAX_BINS) {       // drop the sub-bins of the per-batch plan
+    for (uint32_t w = 0; w < P.nwin; ++w) P.nsub[w] = 1;
+    plan_layout(P);
+  }
+  if (P.bins_per_range * nb > MSM_MAX_BINS) { ctx->err = "multi-batch: too many batches for the MSM plan"; return EDC_ERR_ARG; }
+  const size_t nx_max = (size_t)nb * kstride + nb;
+  const size_t full_max = (N > (size_t)nb * kstride ? N : (size_t)nb * kstride) + nb;
+  rc = ensure_msm(ctx, s, P, msm_entry_capacity(P, N, full_max));
+  if (rc) return rc;
+  if ((size_t)nb * kstride * KEY_ACC_LIMBS > s.mb_cap_acc || nx_max > s.mb_cap_terms || !s.mb_bad) {
+    CK(hipStreamSynchronize(s.st));
+    void* mb[] = {s.mb_acc, s.mb_xpt, s.mb_xrg, s.mb_xscal, s.mb_bad};
+    for (void* p : mb)
+      if (p) (void)hipFree(p);
+    s.mb_acc = nullptr;
+    s.mb_xpt = s.mb_xrg = s.mb_xscal = nullptr;
+    s.mb_bad = nullptr;
+    s.mb_cap_acc = s.mb_cap_terms = 0;
+    const size_t acc = (size_t)kMultiMax * kMultiKeys * KEY_ACC_LIMBS, terms = (size_t)kMultiMax * kMultiKeys + kMultiMax;
+    CK(dalloc(&s.mb_acc, acc));
+    CK(dalloc(&s.mb_xpt, terms));
+    CK(dalloc(&s.mb_xrg, terms));
+    CK(dalloc(&s.mb_xscal, terms * 8));
+    CK(dalloc(&s.mb_bad, kMultiMax));
+    s.mb_cap_acc = acc;
+    s.mb_cap_terms = terms;
+  }
+  const uint32_t n = (uint32_t)N;
+  const uint32_t T = (uint32_t)next_pow2(2 * (N < 128 ? 128 : N));
+  if (T > s.cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
+  uint32_t seed[8];
+  seed_words(z_seed, seed);
+  hipStream_t st = s.st;
+  s.timed = false;
+  s.kin = d_k ? d_k : s.k;
+  s.per_sig = per_sig;
+  s.n_batch = n;
+  s.nmulti = nb;
+  launch_init_batch(st, s.flags, per_sig ? (int)n : -1, s.u_acc, s.d_out, per_sig ? nullptr : s.table, per_sig ? 0u : T,
+                    s.counts, P.nbin());
+  if (!per_sig) {
+    const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
+    const uint32_t salt[2] = {(uint32_t)h, (uint32_t)(h >> 32)};
+    launch_keys(st, n, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
+                s.key_index, s.key_acc, s.flags, kstride);
+  }
+  const bool dual = EDC_DUAL_STREAM && s.st2;       // same contract as enqueue_prefix
+  if (dual) {
+    CK(hipEventRecord(s.ev_keys, st));
+    CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
+    launch_decompress(s.st2, n, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
+                      false);
+    CK(hipEventRecord(s.ev_dec, s.st2));
+  }
+  if (!d_k) launch_challenge(st, n, d_vk, d_sig, d_msg, d_off, s.k);
+  launch_multi_coef(st, n, nb, kstride, per_sig, d_sig, s.kin, seed, z_base, s.key_index, s.scal, s.mb_acc, s.u_acc,
+                    s.itembad, s.flags, s.mb_xpt, s.mb_xrg, s.mb_xscal);
+  const MsmTerms terms{n, (uint32_t)n_per, 0u, nb, 1u, s.scal, s.mb_xpt, s.mb_xrg, s.mb_xscal, 0u, per_sig ? 3u : 1u};
+  launch_msm_bin(st, P, terms, (uint32_t)(N + full_max), s.counts, s.offsets, s.cursor, s.entries, s.flags, true);
+  if (dual) CK(hipStreamWaitEvent(st, s.ev_dec, 0));
+  else
+    launch_decompress(st, n, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
+                      false);
+  CK(hipMemsetAsync(s.mb_bad, 0, nb, st));
+  launch_range_prebad(st, n, (uint32_t)n_per, s.itembad, s.itembad + s.cap_n, s.keybad, s.key_index, per_sig, s.mb_bad,
+                      s.flags);
+  launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
+                    s.slice_T);
+  launch_msm_multi_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, s.mb_bad, want_compress, s.d_out, s.h_out);
+  CK(hipGetLastError());
+  s.pending = true;
+  return 0;
+}
+
+// Wait for a multi-batch slot: per batch verdict (EDC_OK / EDC_INVALID_SIGNATURE), optional
+// check8 (nb x 32), partial (nb x 128) and bad flag; returns EDC_INVALID_SIGNATURE if any failed.
+static int finish_multi(edc_ctx* ctx, Slot& s, size_t nb, int* verdicts, uint8_t* check8, uint8_t* partials, int* bad) {
+  if (!s.pending || !s.nmulti) { ctx->err = "no multi-batch pending in this slot"; return EDC_ERR_ARG; }
+  if (nb != s.nmulti) { ctx->err = "multi-batch count differs from the submission"; return EDC_ERR_ARG; }
+  s.pending = false;
+  s.nmulti = 0;
+  CK(hipStreamSynchronize(s.st));
+  const int* h0 = reinterpret_cast<const int*>(s.h_out);
+  if (h0[45]) {
+    ctx->err = "prehashed k is not a canonical scalar (must be < l, as Scalar::from_hash returns)";
+    return EDC_ERR_ARG;
+  }
+  if (s.per_sig) {
+    ctx->ungrouped_run++;
+  } else {
+    ctx->ungrouped_run = 0;
+    ctx->have_key_ratio = true;
+    ctx->last_key_ratio = (double)h0[2] / (double)s.n_batch;
+  }
+  if (ctx->kc_m) ctx->last_uncached = (uint32_t)h0[44];
+  int any = 0;
+  for (size_t g = 0; g < nb; ++g) {
+    const uint8_t* b = s.h_out + 256 * g;
+    const int v = reinterpret_cast<const int*>(b)[0], bd = reinterpret_cast<const int*>(b)[1];
+    any |= v;
+    if (verdicts) verdicts[g] = v ? EDC_INVALID_SIGNATURE : EDC_OK;
+    if (bad) bad[g] = bd;
+    if (check8) {
+      if (bd) memset(check8 + 32 * g, 0, 32);
+      else memcpy(check8 + 32 * g, b + 16, 32);
+    }
+    if (partials) memcpy(partials + 128 * g, b + 48, 128);
+  }
+  return any ? EDC_INVALID_SIGNATURE : EDC_OK;
+}
+
 // Wait for slot s and harvest its result block (verdict, bad flag, check8, partial).
 static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t partial[128], int* bad_out) {
   if (!s.pending) { ctx->err = "no batch pending in this slot"; return EDC_ERR_ARG; }
+  if (s.nmulti) { ctx->err = "multi-batch ticket: wait with edc_batch_wait_multi"; return EDC_ERR_ARG; }
   s.pending = false;
   CK(hipStreamSynchronize(s.st));
   if (s.timed) {
@@ -802,6 +955,11 @@ void edc_destroy(edc_ctx* ctx) {
     {
       void* in[] = {s.in_vk, s.in_sig, s.in_msg, s.in_off, s.in_idx};
       for (void* p : in)
+        if (p) (void)hipFree(p);
+    }
+    {
+      void* mb[] = {s.mb_acc, s.mb_xpt, s.mb_xrg, s.mb_xscal, s.mb_bad};
+      for (void* p : mb)
         if (p) (void)hipFree(p);
     }
     if (s.flags) (void)hipFree(s.flags);
@@ -919,6 +1077,31 @@ int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t par
   Slot& s = ctx->slot[ticket % ctx->nslots];
   if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
   return finish_batch(ctx, s, check8, partial, bad);
+}
+
+int64_t edc_batch_submit_multi_device(edc_ctx* ctx, size_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
+                                      const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t* d_k,
+                                      const uint8_t z_seed[32], uint64_t z_base, int want_check8) {
+  if (!ctx || !z_seed) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  const int64_t ticket = ctx->next_ticket;
+  Slot& s = ctx->slot[ticket % ctx->nslots];
+  if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
+  int rc = enqueue_multi(ctx, s, (uint32_t)(nb <= kMultiMax ? nb : 0), n_per, d_vk, d_sig, d_msg, d_msg_off,
+                         reinterpret_cast<const uint32_t*>(d_k), z_seed, z_base, want_check8 != 0);
+  if (rc) return rc;
+  s.ticket = ticket;
+  ctx->next_ticket++;
+  return ticket;
+}
+
+int edc_batch_wait_multi(edc_ctx* ctx, int64_t ticket, size_t nb, int* verdicts, uint8_t* check8, uint8_t* partials,
+                         int* bad) {
+  if (!ctx || ticket < 0) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  Slot& s = ctx->slot[ticket % ctx->nslots];
+  if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
+  return finish_multi(ctx, s, nb, verdicts, check8, partials, bad);
 }
 
 int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,

@@ -109,6 +109,11 @@ struct MsmTerms {
   const uint32_t* xrg;
   const uint32_t* xscal;
   uint32_t split;                 // batch with split coefficients (msm_num_points_split): all terms short
+  // several batches in one launch (edc_batch_submit_multi_device): bit 0 set = the layout is
+  // resolved on the device from the key grouping (flags): npoint = n (or 2n with one key term per
+  // signature: bit 1 = per signature by the host's choice, or FLAG_OVF), nx = nranges * m + nranges
+  // listed terms, where the host passes nranges in nx
+  uint32_t dyn;
 };
 
 // signed digit of window w (bits <= 16) with carry in/out; top_unsigned keeps the raw value

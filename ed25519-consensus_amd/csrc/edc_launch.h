@@ -14,7 +14,8 @@ void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uin
                        const KeyCacheView& kc, bool split = false);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
-                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags);
+                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags,
+                 uint32_t kcap = 0xFFFFFFFFu);
 // per-signature key terms (no grouping): m = n, key j is signature j's own key (key_rep = null)
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
@@ -27,9 +28,16 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
                        const uint8_t* sig, const uint32_t* k, const uint8_t* zexp, const uint32_t seed[8],
                        uint64_t zbase, const uint32_t* key_index, uint32_t* scal, unsigned long long* key_acc,
                        unsigned long long* u_acc, int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal);
+// several batches in one launch (nr equal ranges of n / nr items, n / nr a multiple of COEF_CHUNK):
+// per-item z and s checks, per-(range, key) sums at g * kstride + key (grouped keys; more than
+// kstride distinct keys must have set FLAG_OVF: launch_keys' kcap), listed key / B terms
+void launch_multi_coef(hipStream_t st, uint32_t n, uint32_t nr, uint32_t kstride, bool per_sig, const uint8_t* sig,
+                       const uint32_t* k, const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index,
+                       uint32_t* scal, unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad,
+                       int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal);
 void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* itembad_r,
                          const uint8_t* keybad,
-                         const uint32_t* key_index, bool per_sig, uint8_t* rbad);
+                         const uint32_t* key_index, bool per_sig, uint8_t* rbad, const int* flags = nullptr);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
 void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const uint8_t* vk, const uint8_t* sig,
                          const uint32_t* k, uint8_t* out_vk, uint8_t* out_sig, uint32_t* out_k);
@@ -54,6 +62,11 @@ void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, 
                      uint32_t* win, int* flags, int want_compress, uint8_t* out, uint8_t* hout = nullptr);
 void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                            uint32_t* win, uint8_t* rverdict);
+// several batches in one launch: per range the window combine, Horner, x8 and identity, one
+// 256-byte result block per range at out + 256 g (and hout + 256 g)
+void launch_msm_multi_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
+                           uint32_t* win, const int* flags, const uint8_t* rbad, int want_compress, uint8_t* out,
+                           uint8_t* hout);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
                     uint8_t* out);
 // 256-byte result block src -> dst (dst may be a peer device's memory)

@@ -20,6 +20,17 @@
 namespace edc {
 
 
+// the multi-batch layout (MsmTerms::dyn) from the batch's key grouping
+__device__ __forceinline__ MsmTerms resolve_terms(MsmTerms T, const int* flags) {
+  if (T.dyn & 1u) {
+    const bool per_sig = (T.dyn & 2u) || flags[FLAG_OVF];
+    const uint32_t nr = T.nx, m = per_sig ? 0u : (uint32_t)flags[FLAG_NKEYS];
+    T.npoint = per_sig ? 2 * T.n : T.n;
+    T.nx = nr * m + nr;
+  }
+  return T;
+}
+
 __device__ __forceinline__ uint32_t terms_count(const MsmTerms& T, const int* flags) {
   if (T.rsize) return T.npoint + T.nx;
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
@@ -77,6 +88,7 @@ __global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32
   const uint32_t nbin = P.nbin();
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
+  T = resolve_terms(T, flags);
   const uint32_t cnt = terms_count(T, flags);
   const uint32_t t0 = blockIdx.x * per_block;
   for (uint32_t u = threadIdx.x; u < per_block; u += blockDim.x) {
@@ -168,6 +180,7 @@ __global__ void __launch_bounds__(SCATTER_THREADS) k_msm_scatter(MsmPlan P, MsmT
   uint2* stage = reinterpret_cast<uint2*>(smem_hist + 3 * nbin + (nbin & 1));  // 8-byte aligned
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
+  T = resolve_terms(T, flags);
   const uint32_t cnt = terms_count(T, flags);
   // pass 1: local counts (recomputed in pass 2 from the same digits)
   scatter_terms(SB, cnt, [&](uint32_t t) {
@@ -849,6 +862,44 @@ __global__ void __launch_bounds__(64) k_msm_range_final(MsmPlan P, const uint32_
   if (threadIdx.x == 0) rverdict[g] = ge_is_identity(ld_ext(res + EXT_WORDS)) ? 0 : 1;
 }
 
+// Several batches in one launch: range g's Horner, x8, identity -> result block g (the layout of
+// k_msm_final's, at out + 256 g and, when given, hout + 256 g): verdict, bad flag (its range's
+// failed decodes / s checks, rbad[g]), check8, partial point. One workgroup per range.
+__global__ void __launch_bounds__(64) k_msm_multi_final(MsmPlan P, const uint32_t* __restrict__ slice_W,
+                                                        const uint32_t* __restrict__ win, const int* __restrict__ flags,
+                                                        const uint8_t* __restrict__ rbad, int want_compress,
+                                                        uint8_t* __restrict__ out, uint8_t* __restrict__ hout) {
+  __shared__ uint32_t cached[MSM_MAX_WIN * 64];
+  __shared__ uint32_t res[2 * EXT_WORDS];
+  __shared__ uint32_t blk[64];
+  const uint32_t g = blockIdx.x;
+  if (g >= P.nranges) return;
+  __builtin_amdgcn_s_setprio(3);
+  const RowCtx c = row_ctx();
+  blk[threadIdx.x] = 0;
+  cache_windows(c, P, g, slice_W, win, cached, 0, 1);
+  horner_row(c, P, g, slice_W, win, cached, res);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
+    ext_to_canonical_bytes(acc, reinterpret_cast<uint8_t*>(blk) + 48);
+    const int bad = rbad[g] ? 1 : 0;
+    blk[0] = (!bad && ge_is_identity(c8)) ? 0u : 1u;
+    blk[1] = (uint32_t)bad;
+    blk[2] = (uint32_t)flags[FLAG_NKEYS];
+    blk[3] = (uint32_t)flags[FLAG_OVF];
+    blk[44] = (uint32_t)flags[FLAG_UNCACHED];
+    blk[45] = (uint32_t)flags[FLAG_KARG];
+    if (want_compress) ge_compress(c8, blk + 4);
+  }
+  __syncthreads();
+  reinterpret_cast<uint32_t*>(out + 256 * (size_t)g)[threadIdx.x] = blk[threadIdx.x];
+  if (hout) {
+    reinterpret_cast<uint32_t*>(hout + 256 * (size_t)g)[threadIdx.x] = blk[threadIdx.x];
+    __threadfence_system();
+  }
+}
+
 // combine G partial check points (canonical 128-byte records) from G shards
 __global__ void k_combine(uint32_t g, const uint8_t* __restrict__ partials, int bad,
                           int want_compress, uint8_t* __restrict__ out) {
@@ -995,6 +1046,15 @@ void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* sli
   if (plan_multi(P))
     hipLaunchKernelGGL(k_msm_window, dim3(P.nwin * P.nranges), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
   hipLaunchKernelGGL(k_msm_range_final, dim3(P.nranges), dim3(64), 0, st, P, slice_W, win, rverdict);
+}
+
+void launch_msm_multi_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
+                           uint32_t* win, const int* flags, const uint8_t* rbad, int want_compress, uint8_t* out,
+                           uint8_t* hout) {
+  if (plan_multi(P))
+    hipLaunchKernelGGL(k_msm_window, dim3(P.nwin * P.nranges), dim3(256), kReduceLds, st, P, slice_W, slice_T, win);
+  hipLaunchKernelGGL(k_msm_multi_final, dim3(P.nranges), dim3(64), 0, st, P, slice_W, win, flags, rbad, want_compress,
+                     out, hout);
 }
 
 void launch_copy_block(hipStream_t st, const uint8_t* src, uint8_t* dst) {

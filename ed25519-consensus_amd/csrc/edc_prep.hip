@@ -19,6 +19,120 @@ constexpr int SHA_THREADS = 256;  // items regrouped per workgroup
 #ifndef EDC_SHA_OCC
 #define EDC_SHA_OCC 4
 #endif
+#ifndef EDC_SHA_STAGED
+#define EDC_SHA_STAGED 1
+#endif
+
+// ---- SHA-512 over R || A || M with the message staged through LDS (k_challenge) ----
+// Each block's message bytes (a 128-byte window; 64 bytes in block 0, after R || A) are fetched
+// for the whole wave by LDS-DMA (global_load_lds_dwordx4) before they are needed: instruction c
+// moves every lane's c-th 16-byte chunk of its window (16-byte aligned, 9 chunks cover 128 bytes
+// at any alignment) into column `lane` of row c of the wave's buffer, so no VGPR holds the
+// loads and the next block's chunks travel while the current block compresses. Chunks past the
+// message's last 16-byte chunk come from a zero line, so the window already holds the padding's
+// zeros; the lane whose message ends in the window fixes the one chunk that straddles the end
+// (marker 0x80, zeros after it) in its own column. The words are then assembled from LDS dwords
+// with one funnel shift (v_alignbyte) and one byte swap (v_perm) per half: ~5 VALU per word,
+// where the per-lane global walk (three clamped dword loads per word, each waited on at once)
+// cost ~45 and serialized the memory latency word by word.
+constexpr int SHA_WIN_CHUNKS = 9;
+__device__ __attribute__((aligned(16))) uint32_t g_sha_zero[4];
+
+__device__ __forceinline__ void sha_dma16(const void* gsrc, uint32_t* lds_row) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_row, 16, 0, 0);
+}
+
+// dword x of lane's window column (row = 16-byte chunk, 256 dwords per row)
+__device__ __forceinline__ uint32_t* sha_col(uint32_t* wbuf, uint32_t lane, uint32_t x) {
+  return wbuf + (x >> 2) * 256 + lane * 4 + (x & 3);
+}
+
+// Issue the DMA of block blk's window (every lane of the wave takes part, live or not).
+__device__ __forceinline__ void sha_stage(uint32_t* wbuf, uintptr_t mbase, uint64_t mlen, uint32_t blk) {
+  const uint64_t w0 = blk ? (uint64_t)blk * 128 - 64 : 0;
+  const uintptr_t S = (mbase + w0) & ~(uintptr_t)15;
+  const uintptr_t last = mlen ? ((mbase + mlen - 1) & ~(uintptr_t)15) : 0;
+#pragma unroll
+  for (int c = 0; c < SHA_WIN_CHUNKS; ++c) {
+    if (blk == 0 && c >= 5) break;                 // block 0: 64 message bytes, 5 chunks
+    const uintptr_t g = S + 16u * c;
+    const void* src = (mlen && g <= last) ? (const void*)g : (const void*)g_sha_zero;
+    sha_dma16(src, wbuf + c * 256);
+  }
+}
+
+// SHA-512(R || A || M) state of item i (lane of a wave whose every lane calls this, live or not).
+__device__ __forceinline__ bool sha_staged_state(uint32_t i, uint32_t n, const uint8_t* __restrict__ vk,
+                                                 const uint8_t* __restrict__ sig, const uint8_t* __restrict__ msg,
+                                                 const uint64_t* __restrict__ off, uint32_t* wbuf, uint64_t h[8]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool live = i < n;
+  const uint64_t o0 = live ? off[i] : 0, mlen = live ? off[i + 1] - o0 : 0;
+  const uint64_t total = 64 + mlen;
+  const uint32_t nblocks = live ? (uint32_t)((total + 17 + 127) / 128) : 0u;
+  uint32_t nb_max = nblocks;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) nb_max = max(nb_max, (uint32_t)__shfl_xor((int)nb_max, d, 64));
+  nb_max = __builtin_amdgcn_readfirstlane(nb_max);
+  const uintptr_t mbase = (uintptr_t)msg + o0;
+  sha512_init(h);
+  sha_stage(wbuf, mbase, mlen, 0);
+#pragma unroll 1
+  for (uint32_t blk = 0; blk < nb_max; ++blk) {
+    const uint64_t w0 = blk ? (uint64_t)blk * 128 - 64 : 0;
+    const uint32_t wlen = blk ? 128u : 64u;
+    const uint32_t q0b = (uint32_t)((mbase + w0) & 15);
+    uint64_t w[16];
+    if (blk == 0 && blk < nblocks) {               // R || A: words 0..7, 16-byte aligned rows
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w[t] = load_be64(sig + (size_t)i * 64 + 8 * t);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) w[4 + t] = load_be64(vk + (size_t)i * 32 + 8 * t);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): this block's chunks are in LDS
+    asm volatile("" ::: "memory");
+    // the message ends in this window: marker 0x80 at its end, zeros to the end of that chunk
+    const int64_t e_rel = (int64_t)mlen - (int64_t)w0;
+    if (live && e_rel >= 0 && e_rel < (int64_t)wlen) {
+      const uint32_t pos = q0b + (uint32_t)e_rel, di = pos >> 2, sb = 8 * (pos & 3);
+      uint32_t* p = sha_col(wbuf, lane, di);
+      *p = (*p & ((1u << sb) - 1u)) | (0x80u << sb);
+      const uint32_t rest = 3u - (di & 3u);        // dwords after di in its 16-byte chunk
+      if (rest >= 1) p[1] = 0u;
+      if (rest >= 2) p[2] = 0u;
+      if (rest >= 3) p[3] = 0u;
+    }
+    // window dwords from the one holding byte q0b: four base pointers (x = b0 + 4j + r)
+    const uint32_t b0 = q0b >> 2, sh = q0b & 3;
+    uint32_t* P0 = sha_col(wbuf, lane, b0), *P1 = sha_col(wbuf, lane, b0 + 1);
+    uint32_t* P2 = sha_col(wbuf, lane, b0 + 2), *P3 = sha_col(wbuf, lane, b0 + 3);
+    auto dw = [&](int k) -> uint32_t {
+      const int j = k >> 2, r = k & 3;
+      return (r == 0 ? P0 : r == 1 ? P1 : r == 2 ? P2 : P3)[j * 256];
+    };
+    const int t0 = blk ? 0 : 8;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (t < t0) continue;
+      const int k = 2 * (t - t0);
+      const uint32_t d0 = dw(k), d1 = dw(k + 1), d2 = dw(k + 2);
+      const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      w[t] = mk64(bswap32(hi), bswap32(lo));
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): the window is read before it is refilled
+    asm volatile("" ::: "memory");
+    if (blk + 1 < nb_max) sha_stage(wbuf, mbase, mlen, blk + 1);
+    if (blk < nblocks) {
+      if (blk == nblocks - 1) {
+        w[14] = 0;                                  // bit-length high word (messages < 2^61 bytes)
+        w[15] = total << 3;
+      }
+      sha512_compress(h, w);
+    }
+  }
+  return live;
+}
 __global__ void __launch_bounds__(SHA_THREADS, EDC_SHA_OCC) k_challenge(uint32_t n, const uint8_t* __restrict__ vk,
                                                    const uint8_t* __restrict__ sig,
                                                    const uint8_t* __restrict__ msg,
@@ -49,11 +163,24 @@ __global__ void __launch_bounds__(SHA_THREADS, EDC_SHA_OCC) k_challenge(uint32_t
   order[cls_base[cls] + rank] = i0;
   __syncthreads();
   const uint32_t i = order[t];
+#if EDC_SHA_STAGED
+  __shared__ __attribute__((aligned(16))) uint32_t win[SHA_THREADS / 64][SHA_WIN_CHUNKS * 256];
+  uint64_t h[8];
+  const bool live = sha_staged_state(i, n, vk, sig, msg, off, win[t >> 6], h);
+  if (!live) return;
+  uint32_t x[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    x[2 * j] = bswap32((uint32_t)(h[j] >> 32));
+    x[2 * j + 1] = bswap32((uint32_t)h[j]);
+  }
+#else
   if (i >= n) return;
   uint64_t o0 = off[i], o1 = off[i + 1];
   sha_src s{sig + (size_t)i * 64, vk + (size_t)i * 32, msg + o0, o1 - o0};
   uint32_t x[16];
   sha512_src_le_words(s, x);
+#endif
   sc k = sc_reduce_wide(x);
   uint4* kp = reinterpret_cast<uint4*>(k_out + (size_t)i * 8);
   kp[0] = make_uint4(k.v[0], k.v[1], k.v[2], k.v[3]);
@@ -234,14 +361,22 @@ __global__ void __launch_bounds__(256) k_key_seed(uint32_t n, const uint8_t* __r
 }
 
 // dense key index per signature; after a probe overflow the batch falls back to one key term
-// per signature (m = n), decided here on the device
+// per signature (m = n), decided here on the device. kcap: the most distinct keys the caller's
+// per-(range, key) sums have room for (several batches in one launch); more also fall back.
 __global__ void __launch_bounds__(256) k_key_index(uint32_t n, const uint32_t* __restrict__ key_slot_of_sig,
                                                    const uint32_t* __restrict__ slot_key,
-                                                   uint32_t* __restrict__ key_index, int* __restrict__ flags) {
+                                                   uint32_t* __restrict__ key_index, int* __restrict__ flags,
+                                                   uint32_t kcap) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (flags[FLAG_OVF]) {
-    if (i == 0) flags[FLAG_NKEYS] = (int)n;
+  // every lane decides from the values k_key_insert left: FLAG_NKEYS is only rewritten to n,
+  // which is > kcap whenever the original count was
+  const bool over = (uint32_t)flags[FLAG_NKEYS] > kcap;
+  if (flags[FLAG_OVF] || over) {
+    if (i == 0) {
+      flags[FLAG_OVF] = 1;
+      flags[FLAG_NKEYS] = (int)n;
+    }
     return;
   }
   key_index[i] = slot_key[key_slot_of_sig[i]];
@@ -343,7 +478,7 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
       const bool s_bad = !sc_is_canonical(sw);
       bad |= s_bad;
       karg |= !sc_is_canonical(kw);   // k from Scalar::from_hash is < l; only a prehashed caller can break it
-      if (!rsize) itembad[i] = s_bad ? ITEM_BAD_S : 0;   // first writer of the batch's per-item bits
+      if (itembad) itembad[i] = s_bad ? ITEM_BAD_S : 0;   // first writer of the batch's per-item bits
       uint32_t u[PL], v[PL];
       mul_128x256(z, sw, u);
       mul_128x256(z, kw, v);
@@ -549,15 +684,45 @@ __global__ void __launch_bounds__(256) k_range_terms(uint32_t n, uint32_t nrange
   }
 }
 
+// Several batches in one launch (nr equal ranges of n / nr items): listed MSM terms from the
+// per-(range, key) sums, laid out key-major per range (sum of key j in range g at g * kstride + j,
+// so the host needs no key count): q < nr m -> (n+1+j, g, sum z k), then one B term per range.
+// m comes from the batch's key grouping (0 with one key term per signature: those terms are
+// point terms, k_coef wrote their scalars).
+__global__ void __launch_bounds__(256) k_multi_terms(uint32_t n, uint32_t nr, uint32_t kstride,
+                                                     const unsigned long long* __restrict__ key_acc,
+                                                     const unsigned long long* __restrict__ u_acc,
+                                                     const int* __restrict__ flags, int per_sig_host,
+                                                     uint32_t* __restrict__ xpt, uint32_t* __restrict__ xrg,
+                                                     uint32_t* __restrict__ xscal) {
+  const bool per_sig = per_sig_host || flags[FLAG_OVF];
+  const uint32_t m = per_sig ? 0u : (uint32_t)flags[FLAG_NKEYS];
+  const uint32_t npair = nr * m;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < npair + nr; q += gridDim.x * blockDim.x) {
+    if (q < npair) {
+      const uint32_t g = q / m, j = q - g * m;
+      xpt[q] = 1 + n + j;
+      xrg[q] = g;
+      store_scalar(xscal, q, reduce_limb_sums(key_acc + ((size_t)g * kstride + j) * PL));
+    } else {
+      const uint32_t g = q - npair;
+      xpt[q] = 0;
+      xrg[q] = g;
+      store_scalar(xscal, q, sc_sub(sc_zero(), reduce_limb_sums(u_acc + (size_t)g * PL)));
+    }
+  }
+}
+
 // Range mode: rbad[g] = 1 iff range g holds an item whose R or s failed, or whose key failed to
 // decode (such ranges are verified item by item whatever their partial point).
 __global__ void __launch_bounds__(256) k_range_prebad(uint32_t n, uint32_t rsize, const uint8_t* __restrict__ itembad,
                                                       const uint8_t* __restrict__ itembad_r,
                                                       const uint8_t* __restrict__ keybad,
-                                                      const uint32_t* __restrict__ key_index, int per_sig,
-                                                      uint8_t* __restrict__ rbad) {
+                                                      const uint32_t* __restrict__ key_index, int per_sig_host,
+                                                      const int* __restrict__ flags, uint8_t* __restrict__ rbad) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const bool per_sig = per_sig_host || (flags && flags[FLAG_OVF]);
   if (itembad[i] || itembad_r[i] || keybad[per_sig ? i : key_index[i]]) rbad[i / rsize] = 1;
 }
 
@@ -590,7 +755,7 @@ void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uin
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
-                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags) {
+                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags, uint32_t kcap) {
   if (!n) return;
   const uint32_t cap = force_overflow ? 0u : KEY_PROBE_CAP;
   if (n > 4 * KEY_SEED_SAMPLE) {
@@ -600,7 +765,7 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
   hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt[0], salt[1], cap,
                      slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
-                     key_index, flags);
+                     key_index, flags, kcap);
 }
 // One launch for the per-batch resets (flags, global coefficient sums, result block, key table,
 // MSM bin counts) instead of five runtime fills: each fill is a launch of its own, ~8 us apiece in
@@ -662,12 +827,27 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }
+void launch_multi_coef(hipStream_t st, uint32_t n, uint32_t nr, uint32_t kstride, bool per_sig, const uint8_t* sig,
+                       const uint32_t* k, const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index,
+                       uint32_t* scal, unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad,
+                       int* flags, uint32_t* xpt, uint32_t* xrg, uint32_t* xscal) {
+  seed8 s;
+  for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
+  if (!per_sig) (void)hipMemsetAsync(key_acc, 0, (size_t)nr * kstride * PL * sizeof(unsigned long long), st);
+  (void)hipMemsetAsync(u_acc, 0, (size_t)nr * PL * sizeof(unsigned long long), st);
+  if (n)
+    hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, (const uint8_t*)nullptr, s, zbase,
+                       key_index, scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, n / nr, kstride,
+                       (uint32_t*)nullptr, 0);
+  hipLaunchKernelGGL(k_multi_terms, dim3(grid_cap(cdiv((uint64_t)nr * (per_sig ? 1 : kstride + 1), 256), 1024)),
+                     dim3(256), 0, st, n, nr, kstride, key_acc, u_acc, flags, per_sig ? 1 : 0, xpt, xrg, xscal);
+}
 void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8_t* itembad, const uint8_t* itembad_r,
                          const uint8_t* keybad,
-                         const uint32_t* key_index, bool per_sig, uint8_t* rbad) {
+                         const uint32_t* key_index, bool per_sig, uint8_t* rbad, const int* flags) {
   if (n)
     hipLaunchKernelGGL(k_range_prebad, dim3(cdiv(n, 256)), dim3(256), 0, st, n, rsize, itembad, itembad_r, keybad,
-                       key_index, per_sig ? 1 : 0, rbad);
+                       key_index, per_sig ? 1 : 0, flags, rbad);
 }
 // Key-indexed host submissions (edc_batch_submit_indexed): item i's raw key bytes from the key
 // cache, vk_out[i] = keys[reg[key_idx[i]]] (indices were range-checked on the host), so the

@@ -96,6 +96,26 @@ int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, con
 int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad);
 
 /*
+ * Several consecutive batches in ONE launch sequence (a node verifying several blocks' votes at
+ * once, or one GPU's shards of consecutive blocks; reference src/batch.rs:149-217 once per batch):
+ * nb (1..16) batches of n_per items each (n_per a multiple of 2048), back to back in device
+ * memory -- batch b is items [b n_per, (b+1) n_per) of d_vk / d_sig and of the message arena's
+ * nb n_per + 1 offsets (or of d_k: nb n_per prehashed challenges, messages unused, d_msg /
+ * d_msg_off may be NULL). Batch b's z are drawn at global indices z_base + b n_per + i, so its
+ * verdict, bad flag, check8 and partial equal edc_batch_verify_device / edc_batch_partial_device
+ * of batch b alone at z_base + b n_per. Every per-item kernel runs once over all nb n_per items
+ * and the MSM is range-tagged (one range per batch), so small batches fill the GPU like one
+ * large batch. Waited with edc_batch_wait_multi (same ticket rules as edc_batch_submit_device):
+ * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32, needs want_check8),
+ * partials (nb x 128) and bad flags (nb); returns EDC_INVALID_SIGNATURE if any batch failed.
+ */
+int64_t edc_batch_submit_multi_device(edc_ctx* ctx, size_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
+                                      const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t* d_k,
+                                      const uint8_t z_seed[32], uint64_t z_base, int want_check8);
+int edc_batch_wait_multi(edc_ctx* ctx, int64_t ticket, size_t nb, int* verdicts, uint8_t* check8, uint8_t* partials,
+                         int* bad);
+
+/*
  * Host-buffer form of edc_batch_submit_device (replaces src/batch.rs:149 `Verifier::verify` for a
  * caller streaming consecutive batches from host memory): the inputs are copied into the slot's
  * own device buffers on the slot's stream, so the PCIe transfer of this batch overlaps the kernels

@@ -799,13 +799,14 @@ int oc_combine_affine(size_t g, const uint8_t* parts, uint8_t check8[32]) {
 
 /* Full-size oracle check of a GPU batch (tests only): the batch equation is linear and z is drawn
    at global queue indices, so `parts` contiguous ranges, each one oc_batch_verify_range at
-   z_base = its start (one thread each), give partial points whose sum is the whole batch's check
+   z_base + its start (one thread each), give partial points whose sum is the whole batch's check
    point. partials: parts x 64 bytes (affine x || y); rcs[g] = OC_OK / OC_INVALID_SIGNATURE of the
    range alone, evaluated[g] = 0 when the range was rejected before its MSM (undecodable / s >= l). */
 typedef struct {
   size_t lo, hi;
   const uint8_t *vk, *sig, *msg, *seed;
   const uint64_t* off;
+  uint64_t z_base;
   uint8_t* partial;
   int rc, evaluated;
 } pjob;
@@ -818,7 +819,7 @@ static void* pworker(void* p) {
   uint8_t c8[32];
   memset(c8, 0, 32);
   j->rc = oc_batch_verify_range(n, j->vk + 32 * j->lo, j->sig + 64 * j->lo, j->msg + j->off[j->lo], o, j->seed, NULL,
-                                j->lo, c8, j->partial);
+                                j->z_base + j->lo, c8, j->partial);
   static const uint8_t zero[32] = {0};
   j->evaluated = memcmp(c8, zero, 32) != 0;
   free(o);
@@ -826,7 +827,8 @@ static void* pworker(void* p) {
 }
 
 int oc_partials_parallel(size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg, const uint64_t* off,
-                         const uint8_t z_seed[32], int parts, uint8_t* partials, int* rcs, int* evaluated) {
+                         const uint8_t z_seed[32], int parts, uint64_t z_base, uint8_t* partials, int* rcs,
+                         int* evaluated) {
   oc_init_once();
   if (parts < 1) return -1;
   pjob* jobs = (pjob*)calloc((size_t)parts, sizeof(pjob));
@@ -835,6 +837,7 @@ int oc_partials_parallel(size_t n, const uint8_t* vk, const uint8_t* sig, const 
     jobs[g].lo = n * (size_t)g / (size_t)parts;
     jobs[g].hi = n * (size_t)(g + 1) / (size_t)parts;
     jobs[g].vk = vk; jobs[g].sig = sig; jobs[g].msg = msg; jobs[g].off = off; jobs[g].seed = z_seed;
+    jobs[g].z_base = z_base;
     jobs[g].partial = partials + 64 * (size_t)g;
     memset(jobs[g].partial, 0, 64);
     pthread_create(&th[g], NULL, pworker, &jobs[g]);

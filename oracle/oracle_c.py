@@ -23,7 +23,7 @@ def lib():
                                             ctypes.c_void_p]
         L.oc_verify.argtypes = [c_p, c_p, c_p, c_sz]
         L.oc_combine_affine.argtypes = [c_sz, c_p, ctypes.c_void_p]
-        L.oc_partials_parallel.argtypes = [c_sz, c_p, c_p, c_p, u64p, c_p, ctypes.c_int, ctypes.c_void_p,
+        L.oc_partials_parallel.argtypes = [c_sz, c_p, c_p, c_p, u64p, c_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.oc_baseline.restype = ctypes.c_double
         L.oc_baseline.argtypes = [c_sz, c_p, c_p, c_p, u64p, ctypes.c_int, c_sz, ctypes.POINTER(ctypes.c_int)]
@@ -73,7 +73,7 @@ def combine_affine(parts):
     return rc, c8.raw
 
 
-def batch_verify_parallel(vk, sig, msg, offs, z_seed, parts=None):
+def batch_verify_parallel(vk, sig, msg, offs, z_seed, parts=None, z_base=0):
     """Whole-batch (code, check8) of a LARGE batch given as flat byte strings (vk n*32, sig n*64,
     the message arena and n+1 offsets) on all host threads: contiguous ranges at global z indices,
     one oc_batch_verify_range each, partial points summed by oc_combine_affine. check8 is None when
@@ -85,7 +85,8 @@ def batch_verify_parallel(vk, sig, msg, offs, z_seed, parts=None):
     buf = ctypes.create_string_buffer(64 * parts)
     rcs, ev = (ctypes.c_int * parts)(), (ctypes.c_int * parts)()
     t0 = time.perf_counter()
-    rc = lib().oc_partials_parallel(n, vk or b"\0", sig or b"\0", msg or b"\0", o, bytes(z_seed), parts, buf, rcs, ev)
+    rc = lib().oc_partials_parallel(n, vk or b"\0", sig or b"\0", msg or b"\0", o, bytes(z_seed), parts, z_base, buf,
+                                    rcs, ev)
     assert rc == 0
     if not all(ev):
         return 1, None, time.perf_counter() - t0

@@ -85,3 +85,50 @@ def test_variable_length_shards_recombine(engine, oracle_c):
             bad_any |= flag.value
         code, c8 = engine.combine_partials(parts, bad_any)
         assert code == exp_code and c8 == exp_c8, nshards
+
+
+def test_message_window_edges_every_alignment(engine):
+    """The LDS-staged message windows of k_challenge at every padding boundary and every arena
+    alignment: messages of 0..400 bytes (1 to 4 SHA-512 blocks: every position of the end marker
+    and of the length words), the arena placed at byte offsets 0..15 of a device buffer and ending
+    at the buffer's last byte. Each item is signed over its message, so the per-item path
+    (edc_verify_each_device: SHA-512 on the device, then the single verification) accepts it only
+    if k = H(R||A||M) was hashed exactly; the batch over the same arena is Ok with the identity."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    rnd = random.Random(401)
+    lens = list(range(0, 401))
+    msgs = [rnd.randbytes(n) for n in lens]
+    seeds = [rnd.randbytes(32) for _ in range(8)]
+    vks, sigs = engine.sign(seeds, msgs, seed_index=[i % 8 for i in range(len(msgs))])
+    n = len(msgs)
+    offs = [0]
+    for m in msgs:
+        offs.append(offs[-1] + len(m))
+    arena = b"".join(msgs)
+    d_vk = torch.tensor(list(b"".join(vks)), dtype=torch.uint8, device=dev)
+    d_sig = torch.tensor(list(b"".join(sigs)), dtype=torch.uint8, device=dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    lib = engine.lib
+    for shift in range(16):
+        buf = torch.tensor(list(bytes([0xA5]) * shift + arena), dtype=torch.uint8, device=dev)  # arena ends at the last byte
+        out = torch.zeros(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        assert lib.edc_verify_each_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), buf.data_ptr() + shift,
+                                          d_off.data_ptr(), out.data_ptr()) == 0
+        assert out.cpu().tolist() == [0] * n, shift
+        c8 = ctypes.create_string_buffer(32)
+        assert lib.edc_batch_verify_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), buf.data_ptr() + shift,
+                                           d_off.data_ptr(), bytes(32), 0, None, c8) == 0, shift
+        assert c8.raw == bytes([1]) + bytes(31)
+    # and one altered byte in every message is caught item by item
+    bad = bytearray(arena)
+    for i in range(n):
+        if lens[i]:
+            bad[offs[i] + rnd.randrange(lens[i])] ^= 0x01
+    buf = torch.tensor(list(bad), dtype=torch.uint8, device=dev)
+    out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    assert lib.edc_verify_each_device(engine.ctx, n, d_vk.data_ptr(), d_sig.data_ptr(), buf.data_ptr(),
+                                      d_off.data_ptr(), out.data_ptr()) == 0
+    assert out.cpu().tolist() == [0] + [1] * (n - 1)
