@@ -33,6 +33,10 @@ ALG_MAD_PER_SIG_DISTINCT = 2 * 11480 + 24 * 448       # configs[1]/[4]: distinct
 # 35.0 T/s sustained by tools/microbench/valu_rates.hip, profiles/r01_valu_rates.txt)
 PEAK_TMAD = 256 * 4 * 32 * 2.4e9 / 2 / 1e12
 HBM_PEAK_GBS = 8000.0
+# SHA-512 compression per block and lane: 80 x (7 x 64-bit + 20 x 32-bit) + 64 x (3 x 64-bit + 14 x 32-bit)
+SHA_VALU_PER_BLOCK = 80 * 27 + 64 * 17
+SHA_CYCLES_PER_BLOCK = 80 * (7 * 4.1 + 20 * 2.3) + 64 * (3 * 4.1 + 14 * 2.3)   # per wave, per SIMD
+SHA_PEAK_BLOCKS = 1024 * 2.4e9 / SHA_CYCLES_PER_BLOCK * 64
 
 
 def load_pkg():
@@ -387,6 +391,9 @@ def main():
     lib.edc_set_timing(eng.ctx, 0)
     pipe_dec_ms = sum(pipe_ms[max(4, args.inflight):]) / max(1, len(pipe_ms) - max(4, args.inflight))
     phases = {names[i]: round(acc[i], 4) for i in range(7)}
+    # SHA-512 blocks of the instrumented batch (R || A || M, 17 bytes of padding + length)
+    lens = (off[1:n + 1] - off[:n]).to(torch.int64)
+    sha_blocks = int(((64 + lens + 17 + 127) // 128).sum().item())
 
     if rank == 0:
         total = n * nmb * world * args.steps    # strong scaling: n * world == --n
@@ -462,6 +469,18 @@ def main():
                          "measured": f"HIP events on the slot stream around each launch, {max(1, args.profile_steps)} "
                                      "instrumented batches run one at a time after the timed region "
                                      "(rocprof cross-check: profiles/r01_kernel_stats_inflight1.csv)"},
+            # k_challenge against its own issue bound: per 128-byte block and lane, 80 rounds of 7
+            # v_lshl_add_u64 + 20 32-bit VALU (12 v_alignbit, 8 v_bitop3) and 64 schedule steps of
+            # 3 + 14 (ISA of the compression loop, tools: llvm-objdump of libedc.so), priced at the
+            # measured issue costs (64-bit VOP3 4.1, 32-bit 2.3 cycles per wave-instruction per SIMD,
+            # profiles/r01_valu_rates.txt) at the nominal 2.4 GHz over 1024 SIMDs x 64 lanes
+            "roofline_sha512": {"kernel": "k_challenge", "blocks_per_launch": sha_blocks,
+                                "avg_launch_ms": phases["challenge_sha512"],
+                                "achieved_blocks_per_s": round(sha_blocks / (phases["challenge_sha512"] * 1e-3), 1),
+                                "peak_blocks_per_s": round(SHA_PEAK_BLOCKS, 1),
+                                "frac": round(sha_blocks / (phases["challenge_sha512"] * 1e-3) / SHA_PEAK_BLOCKS, 4),
+                                "valu_per_block": SHA_VALU_PER_BLOCK, "bound": "valu issue (integer)"}
+            if phases["challenge_sha512"] > 0 else None,
             "hbm_view": ({"achieved_gbs": round(traffic / (dom_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
                           "frac": round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if traffic else None),
             "phases_ms": phases,

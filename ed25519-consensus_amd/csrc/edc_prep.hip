@@ -53,11 +53,14 @@ __device__ __forceinline__ void sha_stage(uint32_t* wbuf, uintptr_t mbase, uint6
   const uint64_t w0 = blk ? (uint64_t)blk * 128 - 64 : 0;
   const uintptr_t S = (mbase + w0) & ~(uintptr_t)15;
   const uintptr_t last = mlen ? ((mbase + mlen - 1) & ~(uintptr_t)15) : 0;
+  // a window that starts at or past the message's end is all padding: every chunk zero (its first
+  // chunk may still be the message's last one, whose bytes past the end are not zero)
+  const bool inside = mlen > w0;
 #pragma unroll
   for (int c = 0; c < SHA_WIN_CHUNKS; ++c) {
     if (blk == 0 && c >= 5) break;                 // block 0: 64 message bytes, 5 chunks
     const uintptr_t g = S + 16u * c;
-    const void* src = (mlen && g <= last) ? (const void*)g : (const void*)g_sha_zero;
+    const void* src = (inside && g <= last) ? (const void*)g : (const void*)g_sha_zero;
     sha_dma16(src, wbuf + c * 256);
   }
 }

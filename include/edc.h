@@ -12,9 +12,11 @@
  *  - Items are in QUEUE order. vk: n*32 bytes, sig: n*64 bytes (R || s), messages are one
  *    arena `msg` with n+1 offsets (message i = msg[msg_off[i] .. msg_off[i+1])).
  *  - Device-resident inputs (the *_device entries): vk / sig / k arrays 16-byte aligned; the
- *    message arena may be read up to the next 4-byte boundary after the last message byte (the
- *    SHA-512 kernel loads whole aligned dwords), so that many bytes past it must be mapped. Device
- *    allocations (hipMalloc, torch tensors) always satisfy both; host buffers have no such rule.
+ *    message arena is read in whole aligned 16-byte chunks (the SHA-512 kernel stages each
+ *    message through LDS by DMA), i.e. from the 16-byte boundary at or before a message's first
+ *    byte to the one after its last byte; those bytes must be mapped (they are never used).
+ *    Device allocations (hipMalloc, torch tensors) always satisfy both, as such chunks never cross
+ *    a page; host buffers have no such rule (they are staged into the context's own buffers).
  *  - z_i = u128::from_le_bytes(ChaCha20Rng::from_seed(z_seed) keystream[16(z_base+i) ..]),
  *    i.e. gen_u128 (reference src/batch.rs:64-68) drawn in queue order. Batch verification is
  *    sound only when z is unpredictable to the signers: z_seed must come from a CSPRNG, fresh for

@@ -68,3 +68,26 @@ def test_no_gpu_means_loud_failure(edc):
         raise AssertionError("Engine must refuse to run without a GPU")
     except edc.EngineError:
         pass
+
+
+def test_prehashed_item_surface(edc):
+    """batch.Item as the reference stores it ({vk_bytes, sig, k}, src/batch.rs:76-80): built from
+    the message (k hashed later, in one launch) or from k alone; neither is an error."""
+    vk, sig = bytes(32), bytes(64)
+    it = edc.batch.Item.prehashed(vk, sig, bytes(range(32)))
+    assert it.k == bytes(range(32)) and it._msg is None
+    assert edc.batch.Item(vk, sig, b"m").k is None
+    try:
+        edc.batch.Item(vk, sig)
+        raise AssertionError("expected ValueError")
+    except ValueError:
+        pass
+    try:
+        edc.batch.Item.prehashed(vk, sig, bytes(31))
+        raise AssertionError("expected InvalidSliceLength")
+    except edc.InvalidSliceLength:
+        pass
+    v = edc.batch.Verifier()
+    v.queue(it)
+    v.queue((vk, sig, b"x"))
+    assert v.batch_size == 2

@@ -14,6 +14,7 @@
 #   fallback         tools/fallback_bench.py (configs[3])    host  tools/host_bench.py
 #   small            tools/smallbatch_bench.py               multi tools/multi_bench.py
 #   prof             rocprofv3 kernel-trace stats of the bench, one batch at a time and pipelined
+#   pmc              tools/pmc_passes.sh (VALU / INT / FETCH / WRITE passes; then tools/pmc_summary.py here)
 #   rccl1            forced single-rank RCCL loop (process group + per-batch all-gather)
 #   gloo2            two ranks sharing the GPU over gloo, weak and strong
 #   ab=<v1,v2,..>    alternating A/B of variant builds csrc/libedc_<v>.so ("base" = libedc.so) on
@@ -76,6 +77,7 @@ for step in "$@"; do
     prof)
       run prof1 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline
       run profp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profp -o k -- python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    pmc) run pmc 600 bash tools/pmc_passes.sh ;;
     rccl1) run rccl1 300 env EDC_FORCE_DIST=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
     gloo2)
       run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
