@@ -250,8 +250,13 @@ def main():
     slots = max(1, 16 // sharing)
     nmb = max(1, args.multi)                       # batches per launch sequence
     if args.inflight <= 0:
-        args.inflight = 6 if n * nmb >= (1 << 19) else 16
+        if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh)
+            args.inflight = 3 if n * nmb >= (1 << 20) else 4
+        else:
+            args.inflight = 6 if n >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)
+    if nmb > 1:    # every slot's multi-batch workspace is allocated on its first launch: warm them all
+        args.warmup = max(args.warmup, args.inflight + 1)
     # the context rotates over exactly `inflight` slots, so only that many slot streams (hardware
     # queues) exist beside RCCL's own in a multi-rank run; a build with fewer slots keeps its count
     if eng.lib.edc_set_slots(eng.ctx, args.inflight) < 0 and sharing > 1:

@@ -21,7 +21,7 @@
 #                    AB_CONFIGS (default "c3 n17 c2 c5"), AB_REPS rounds (default 2)
 #   bench=<args>     one bench.py run with these arguments (commas for spaces)
 #   pre              configs[2] with prehashed items (edc_batch_submit_prehashed_device)
-#   m17 | m16        4 consecutive 2^17 vote shards / configs[1] batches per launch (--multi 4)
+#   m17 | m16        8 consecutive 2^17 vote shards / configs[1] batches per launch (--multi 8)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -68,8 +68,8 @@ for step in "$@"; do
     n19) bench_step n19 --n 524288 --steps 40 --warmup 5 --no-cpu-baseline ;;
     bench=*) a=${step#bench=}; bench_step bench ${a//,/ } ;;
     pre) bench_step pre --prehashed --steps 40 --warmup 5 --no-cpu-baseline ;;
-    m17) bench_step m17 --n 131072 --multi 4 --steps 20 --warmup 5 --no-cpu-baseline ;;
-    m16) bench_step m16 --config c2 --multi 4 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    m17) bench_step m17 --n 131072 --multi 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    m16) bench_step m16 --config c2 --multi 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
     fallback) run fallback 300 python3 -u tools/fallback_bench.py ;;
     host) run host 300 python3 -u tools/host_bench.py ;;
     small) run small 300 python3 -u tools/smallbatch_bench.py ;;
