@@ -251,7 +251,7 @@ def main():
     nmb = max(1, args.multi)                       # batches per launch sequence
     if args.inflight <= 0:
         if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh)
-            args.inflight = 3 if n * nmb >= (1 << 20) else 4
+            args.inflight = 3 if n * nmb >= (1 << 19) else 4
         else:
             args.inflight = 6 if n >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)

@@ -1,5 +1,6 @@
 // C ABI (include/edc.h): context, workspace and the orchestration of the batch pipeline.
 // Every entry point cites the reference API it replaces in include/edc.h.
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <random>
@@ -225,8 +226,11 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
 #if EDC_DUAL_STREAM
   // 1: every slot; 2: slot 0 only (the synchronous calls' slot), so the pipelined slots keep one
-  // hardware queue each (past ~16 user queues per GPU the scheduler time-slices them)
-  if (EDC_DUAL_STREAM == 1 || &s == &ctx->slot[0]) {
+  // hardware queue each (past ~16 user queues per GPU the scheduler time-slices them).
+  // EDC_SINGLE_STREAM=1 in the environment (measurement only: kernel traces of one batch at a time
+  // that must not overlap the decode with SHA-512) keeps every slot on one stream.
+  static const bool single_stream = getenv("EDC_SINGLE_STREAM") && getenv("EDC_SINGLE_STREAM")[0] == '1';
+  if (!single_stream && (EDC_DUAL_STREAM == 1 || &s == &ctx->slot[0])) {
     CK(create_slot_stream(ctx->device, &s.st2));
     CK(hipEventCreateWithFlags(&s.ev_keys, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&s.ev_dec, hipEventDisableTiming));

@@ -75,7 +75,7 @@ for step in "$@"; do
     small) run small 300 python3 -u tools/smallbatch_bench.py ;;
     multi) run multi 300 python3 -u tools/multi_bench.py ;;
     prof)
-      run prof1 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline
+      run prof1 300 env EDC_SINGLE_STREAM=1 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline
       run profp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profp -o k -- python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     pmc) run pmc 600 bash tools/pmc_passes.sh ;;
     rccl1) run rccl1 300 env EDC_FORCE_DIST=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;

@@ -3,6 +3,7 @@
 # (counter limits per pass: MI355X_MICROARCH.md), for tools/pmc_summary.py.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export EDC_SINGLE_STREAM=1    # one batch at a time, no decode beside SHA-512 (per-kernel issue fractions)
 mkdir -p gpurun_out
 run() {  # name counters...
   local name=$1; shift
