@@ -433,7 +433,10 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
                                                                    uint32_t* __restrict__ slice_W,
                                                                    uint32_t* __restrict__ slice_T) {
   __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
-  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS];   // row buffers of the 4 waves
+#ifndef EDC_ACC_LDS_PAD
+#define EDC_ACC_LDS_PAD 0   // measurement knob: extra LDS words per workgroup (caps workgroups per CU)
+#endif
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS + EDC_ACC_LDS_PAD];   // row buffers of the 4 waves
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;

@@ -175,10 +175,18 @@ def test_multi_full_size_votes_2_20(engine):
     torch.cuda.synchronize()
     res = _multi(engine, d, nb, n_per, zseed, 0)
     assert res[1] == [0] * 5 + [1] + [0] * 2
-    offs = [0] * (nb * n_per + 1)                 # fixed 120-byte messages
-    offs = [120 * i for i in range(nb * n_per + 1)]
+    offs = [120 * i for i in range(nb * n_per + 1)]   # fixed 120-byte messages
     sc, sc8, _, _ = _single(engine, d, 5, n_per, offs, zseed, 0, torch)
     assert sc == 1 and sc8 == res[2][5]
+    # and the C oracle on that batch alone at its global z offset (all host threads)
+    oc = _oc()
+    lo, hi = 5 * n_per, 6 * n_per
+    hv = vk[32 * lo:32 * hi].cpu().numpy().tobytes()
+    hs = sig[64 * lo:64 * hi].cpu().numpy().tobytes()
+    hm = msg[120 * lo:120 * hi].cpu().numpy().tobytes()
+    code, c8, secs = oc.batch_verify_parallel(hv, hs, hm, [120 * i for i in range(n_per + 1)], zseed, z_base=lo)
+    print(f"\n[multibatch-oracle] 2^17 batch at z offset {lo}: oracle {secs:.2f} s, check8 {c8.hex()}")
+    assert (code, c8) == (1, res[2][5])
 
 
 def test_multi_argument_errors(engine, edc):

@@ -35,6 +35,15 @@ __global__ void __launch_bounds__(256, 4) k_madd(uint32_t* out, uint32_t s) {
   for (int i = 0; i < ITERS / 8; ++i) P = ge_madd(P, q);
   out[blockIdx.x * 256 + threadIdx.x] = P.X.v[0] ^ P.Z.v[8];
 }
+__global__ void __launch_bounds__(256, 4) k_madd_sgn(uint32_t* out, uint32_t s) {
+  ge_p3 P;
+  P.X = seed_fe(s + threadIdx.x); P.Y = seed_fe(s + 1 + threadIdx.x); P.Z = fe_one(); P.T = seed_fe(s + 3);
+  ge_niels q;
+  q.ypx = seed_fe(s ^ blockIdx.x); q.ymx = seed_fe(s + 5); q.xy2d = seed_fe(s + 9);
+  uint32_t bits = s * 2654435761u + threadIdx.x;
+  for (int i = 0; i < ITERS / 8; ++i) P = ge_madd_sgn(P, q, (bits >> (i & 31)) & 1u);
+  out[blockIdx.x * 256 + threadIdx.x] = P.X.v[0] ^ P.Z.v[8];
+}
 __global__ void __launch_bounds__(256, 4) k_dbl(uint32_t* out, uint32_t s) {
   ge_p3 P;
   P.X = seed_fe(s + threadIdx.x); P.Y = seed_fe(s + 1 + threadIdx.x); P.Z = fe_one(); P.T = seed_fe(s + 3);
@@ -57,8 +66,10 @@ int run(const char* name, kfn f, int ops_per_lane, double mads_per_op, uint32_t*
   float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
   double ops = (double)blocks * 256 * ops_per_lane * reps;
   double rate = ops / (ms * 1e-3);
-  printf("%-10s %9.3f G lane-ops/s  %8.2f T v_mad_u64_u32/s issued (%.0f per op)\n", name, rate / 1e9,
-         rate * mads_per_op / 1e12, mads_per_op);
+  // cycles per wave-operation per SIMD at the nominal 2.4 GHz (1024 SIMDs)
+  const double cyc = 1024.0 * 2.4e9 / (rate / 64.0);
+  printf("%-10s %9.3f G lane-ops/s  %8.2f T v_mad_u64_u32/s issued (%.0f per op)  %7.0f cyc/wave-op/SIMD\n", name,
+         rate / 1e9, rate * mads_per_op / 1e12, mads_per_op, cyc);
   return 0;
 }
 
@@ -69,6 +80,7 @@ int main() {
   run("fe_sqr", k_sqr, ITERS, 63, d, blocks);
   run("fe_mul", k_mul, ITERS, 99, d, blocks);
   run("ge_madd", k_madd, ITERS / 8, 7 * 99, d, blocks);
+  run("ge_madd_sgn", k_madd_sgn, ITERS / 8, 7 * 99, d, blocks);
   run("ge_dbl", k_dbl, ITERS / 8, 4 * 63 + 4 * 99, d, blocks);
   CHK(hipFree(d));
   return 0;
