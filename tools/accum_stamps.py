@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--window-bits", type=int, default=0)
     ap.add_argument("--msm-parts", type=int, default=0)
     ap.add_argument("--batches", type=int, default=4)
+    ap.add_argument("--n", type=int, default=0, help="override the config's batch size (e.g. 150: a small call)")
+    ap.add_argument("--keys", type=int, default=-1, help="override the config's validator count (0 = distinct)")
     args = ap.parse_args()
     import torch
     import bench
@@ -30,6 +32,10 @@ def main():
     lib_path = os.path.join(ROOT, "ed25519-consensus_amd", "csrc", "libedc_stamps.so")
     eng = pkg.Engine(0, lib_path=lib_path)
     n, keys, msg_len, desc = bench.CONFIGS[args.config]
+    if args.n:
+        n, desc = args.n, f"{desc}, n overridden to {args.n}"
+    if args.keys >= 0:
+        keys = args.keys
     vk, sig, msg, off = bench.make_workload(pkg, eng, torch, dev, n, keys, msg_len, 0)
     torch.cuda.synchronize()
     lib = eng.lib
