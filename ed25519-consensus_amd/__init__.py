@@ -42,6 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
+    "edc_keycache_add",
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
@@ -184,6 +185,8 @@ def load_library(path=None):
         lib.edc_vk_validate.argtypes = [c_vp, c_sz, c_u8p, c_vp]
         lib.edc_keycache_load.restype = ctypes.c_int64
         lib.edc_keycache_load.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+        lib.edc_keycache_add.restype = ctypes.c_int64
+        lib.edc_keycache_add.argtypes = [c_vp, c_sz, c_u8p, c_vp]
         lib.edc_keycache_clear.argtypes = [c_vp]
         lib.edc_keycache_size.restype = c_sz
         lib.edc_keycache_size.argtypes = [c_vp]
@@ -413,6 +416,16 @@ class Engine:
             u = self._check(self.lib.edc_keycache_load(self.ctx, n, b"".join(encs) or b"\0", ok))
         return u, [bool(b) for b in ok.raw[:n]]
 
+    def keycache_add(self, encs):
+        """Add keys to the context's cache without replacing it (a VerificationKey's decoded point,
+        kept for every later verify: src/verification_key.rs:106-114). Returns (number of distinct
+        keys now cached, per-key ok list)."""
+        n = len(encs)
+        ok = ctypes.create_string_buffer(max(n, 1))
+        with self._lock:
+            u = self._check(self.lib.edc_keycache_add(self.ctx, n, b"".join(encs) or b"\0", ok))
+        return u, [bool(b) for b in ok.raw[:n]]
+
     def set_key_grouping(self, mode):
         """0 auto (default), 1 always group keys, 2 never (one A term per signature), 3 test mode:
         grouping abandoned on the device (the adversarial-key overflow path)."""
@@ -633,29 +646,44 @@ class VerificationKeyBytes:
 
 
 class VerificationKey:
-    """reference src/verification_key.rs:106-258. try_from decodes A on the GPU."""
+    """reference src/verification_key.rs:106-258. try_from decodes A on the GPU once and keeps it:
+    the reference stores minus_A in the object (:111-114, :160-175); here the decoded point and its
+    fixed-base table go into the engine's key cache (edc_keycache_add), where every later verify,
+    batch or fallback of that engine finds them (`cached`). keep_decoded=False only validates."""
 
-    __slots__ = ("A_bytes", "_engine")
+    __slots__ = ("A_bytes", "_engine", "cached")
 
-    def __init__(self, vkb, engine):
+    def __init__(self, vkb, engine, cached=False):
         self.A_bytes = vkb
         self._engine = engine
+        self.cached = cached
 
     @classmethod
-    def try_from(cls, data, engine=None):
-        vkb = data if isinstance(data, VerificationKeyBytes) else VerificationKeyBytes(data)
-        eng = engine or default_engine()
-        if eng.vk_validate([vkb.to_bytes()])[0] != EDC_OK:
-            raise MalformedPublicKey()
-        return cls(vkb, eng)
+    def try_from(cls, data, engine=None, keep_decoded=True):
+        r = cls.try_from_many([data], engine, keep_decoded)[0]
+        if isinstance(r, MalformedPublicKey):
+            raise r
+        return r
 
     @classmethod
-    def try_from_many(cls, keys, engine=None):
-        """Batched key ingestion: [VerificationKey or MalformedPublicKey()] per input, one launch."""
+    def try_from_many(cls, keys, engine=None, keep_decoded=False):
+        """Batched key ingestion: [VerificationKey or MalformedPublicKey()] per input, one launch
+        (keep_decoded: also add the keys to the engine's key cache)."""
         vkbs = [k if isinstance(k, VerificationKeyBytes) else VerificationKeyBytes(k) for k in keys]
         eng = engine or default_engine()
-        codes = eng.vk_validate([v.to_bytes() for v in vkbs])
-        return [cls(v, eng) if c == EDC_OK else MalformedPublicKey() for v, c in zip(vkbs, codes)]
+        encs = [v.to_bytes() for v in vkbs]
+        cached = False
+        if keep_decoded and encs:
+            try:
+                _, oks = eng.keycache_add(encs)
+                codes = [EDC_OK if o else EDC_MALFORMED_PUBLIC_KEY for o in oks]
+                cached = True
+            except EngineError:        # cache full, or batches in flight: validate only
+                codes = eng.vk_validate(encs)
+        else:
+            codes = eng.vk_validate(encs)
+        return [cls(v, eng, cached) if c == EDC_OK else MalformedPublicKey() for v, c in zip(vkbs, codes)]
+
 
     def to_bytes(self):
         return self.A_bytes.to_bytes()

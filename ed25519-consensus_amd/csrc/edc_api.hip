@@ -143,11 +143,16 @@ struct edc_ctx {
   size_t fb_cap_g = 0;
   uint32_t fb_ranges = 32;      // target range count of the grouped fallback
   int fb_bits = 10;             // its window width
-  // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load
+  // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load, grown by
+  // edc_keycache_add (device arrays hold kc_cap keys; the host keeps the key words and ok bytes
+  // to rebuild the hash table and answer duplicates)
   uint32_t *kc_table = nullptr, *kc_keys = nullptr, *kc_comb = nullptr;
   uint8_t* kc_ok = nullptr;
   uint32_t* bcomb = nullptr;    // comb table of B, built with the first cache
-  uint32_t kc_m = 0, kc_tmask = 0;
+  uint32_t kc_m = 0, kc_tmask = 0, kc_cap = 0;
+  uint32_t kc_s0 = 0, kc_s1 = 0;        // table hash key, from `secret`
+  std::vector<uint32_t> kc_words;       // kc_m x 8 raw key words
+  std::vector<uint8_t> kc_okh;          // kc_m decode flags
   uint32_t* kc_reg = nullptr;   // registered position -> cache index (edc_batch_submit_indexed)
   uint32_t kc_reg_m = 0;
   // split coefficients (edc_common.h) while the key cache covers the batches' keys:
@@ -156,8 +161,8 @@ struct edc_ctx {
   uint32_t last_uncached = 0;
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
-    if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr};
-    return KeyCacheView{kc_table, kc_keys, kc_ok, kc_comb, kc_tmask, kc_m, bcomb};
+    if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, 0, 0};
+    return KeyCacheView{kc_table, kc_keys, kc_ok, kc_comb, kc_tmask, kc_m, bcomb, kc_s0, kc_s1};
   }
 };
 
@@ -914,6 +919,9 @@ edc_ctx* edc_create(int device) {
   {
     std::random_device rd;   // OS randomness: the key-grouping hash secret of this context
     ctx->secret = ((uint64_t)rd() << 32) ^ (uint64_t)rd();
+    const uint64_t ks = splitmix64(ctx->secret ^ 0x6B657963616368ull);   // key-cache table hash key
+    ctx->kc_s0 = (uint32_t)ks;
+    ctx->kc_s1 = (uint32_t)(ks >> 32);
   }
   (void)hipGetLastError();   // launch checks below must not see an earlier, unrelated failure
   bool ok = hipSetDevice(device) == hipSuccess && msm_init_device() == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
@@ -938,7 +946,9 @@ static void free_keycache(edc_ctx* ctx) {
   ctx->kc_table = ctx->kc_keys = ctx->kc_comb = ctx->kc_reg = nullptr;
   ctx->kc_reg_m = 0;
   ctx->kc_ok = nullptr;
-  ctx->kc_m = ctx->kc_tmask = 0;
+  ctx->kc_m = ctx->kc_tmask = ctx->kc_cap = 0;
+  ctx->kc_words.clear();
+  ctx->kc_okh.clear();
 }
 
 static int sync_all(edc_ctx* ctx) {
@@ -1550,15 +1560,92 @@ int edc_keycache_clear(edc_ctx* ctx) {
 
 size_t edc_keycache_size(const edc_ctx* ctx) { return ctx ? ctx->kc_m : 0; }
 
-int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok) {
-  if (!ctx || (m && !vk)) return EDC_ERR_ARG;
-  int rc = edc_keycache_clear(ctx);
-  if (rc) return rc;
-  if (!m) return 0;
-  // distinct keys in first-occurrence order (the cache is keyed on raw bytes, like the batch's
-  // HashMap<VerificationKeyBytes, _>, src/batch.rs:114)
+// Appends the distinct new keys `neww` (un x 8 words) to the cache: grows the device arrays
+// (capacity doubling; the cached keys keep their indices), decodes the new keys and builds their
+// comb tables, builds B's comb table with the first key, and rebuilds the hash table over all
+// keys. No batch may be in flight (callers check).
+static int kc_append(edc_ctx* ctx, const std::vector<uint32_t>& neww) {
+  const uint32_t u0 = ctx->kc_m, un = (uint32_t)(neww.size() / 8), u = u0 + un;
+  if (!un) return 0;
+  hipStream_t st = ctx->st();
+  const size_t comb_words = (size_t)COMB_ENTRIES * NIELS_WORDS;
+  if (u > ctx->kc_cap) {
+    uint32_t cap = ctx->kc_cap ? 2 * ctx->kc_cap : 16;
+    while (cap < u) cap *= 2;
+    if (cap > KC_MAX_KEYS) cap = KC_MAX_KEYS;
+    uint32_t *keys = nullptr, *comb = nullptr;
+    uint8_t* okd = nullptr;
+    CK(dalloc(&keys, (size_t)cap * 8));
+    CK(dalloc(&okd, cap));
+    if (hipMalloc(&comb, (size_t)cap * comb_words * sizeof(uint32_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(keys);
+      (void)hipFree(okd);
+      ctx->err = "key cache: out of device memory";
+      return EDC_ERR_NOMEM;
+    }
+    if (u0) {
+      CK(hipMemcpyAsync(keys, ctx->kc_keys, (size_t)u0 * 8 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      CK(hipMemcpyAsync(okd, ctx->kc_ok, u0, hipMemcpyDeviceToDevice, st));
+      CK(hipMemcpyAsync(comb, ctx->kc_comb, (size_t)u0 * comb_words * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      CK(hipStreamSynchronize(st));
+    }
+    if (ctx->kc_keys) (void)hipFree(ctx->kc_keys);
+    if (ctx->kc_ok) (void)hipFree(ctx->kc_ok);
+    if (ctx->kc_comb) (void)hipFree(ctx->kc_comb);
+    ctx->kc_keys = keys;
+    ctx->kc_ok = okd;
+    ctx->kc_comb = comb;
+    ctx->kc_cap = cap;
+  }
+  std::vector<uint32_t> all(ctx->kc_words);   // committed to the context only on success
+  all.insert(all.end(), neww.begin(), neww.end());
+  const uint32_t T = (uint32_t)next_pow2(2 * (size_t)(u < 8 ? 8 : u));
+  std::vector<uint32_t> table(T, KC_EMPTY);
+  for (uint32_t c = 0; c < u; ++c) {
+    uint32_t h = kc_hash(&all[8 * c], ctx->kc_s0, ctx->kc_s1) & (T - 1);
+    while (table[h] != KC_EMPTY) h = (h + 1) & (T - 1);
+    table[h] = c;
+  }
+  if (T - 1 != ctx->kc_tmask || !ctx->kc_table) {
+    if (ctx->kc_table) (void)hipFree(ctx->kc_table);
+    ctx->kc_table = nullptr;
+    CK(dalloc(&ctx->kc_table, T));
+  }
+  uint32_t* ext = nullptr;
+  CK(dalloc(&ext, (size_t)(un + 1) * EXT_WORDS));
+  CK(hipMemcpyAsync(ctx->kc_table, table.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(ctx->kc_keys + (size_t)u0 * 8, neww.data(), neww.size() * sizeof(uint32_t),
+                    hipMemcpyHostToDevice, st));
+  launch_kc_decode(st, un, ctx->kc_keys + (size_t)u0 * 8, ext, ctx->kc_ok + u0);
+  launch_kc_comb(st, un, ext, ctx->kc_comb + (size_t)u0 * comb_words);
+  if (!ctx->bcomb) {
+    CK(dalloc(&ctx->bcomb, comb_words));
+    uint32_t* bext = ext + (size_t)un * EXT_WORDS;
+    launch_kc_basepoint(st, bext);
+    launch_kc_comb(st, 1, bext, ctx->bcomb);
+  }
+  CK(hipGetLastError());
+  std::vector<uint8_t> okn(un);
+  CK(hipMemcpyAsync(okn.data(), ctx->kc_ok + u0, un, hipMemcpyDeviceToHost, st));
+  CK(hipStreamSynchronize(st));
+  (void)hipFree(ext);
+  ctx->kc_words.swap(all);
+  ctx->kc_okh.insert(ctx->kc_okh.end(), okn.begin(), okn.end());
+  ctx->kc_m = u;
+  ctx->kc_tmask = T - 1;
+  ctx->last_uncached = 0;                    // try split coefficients with the new key set
+  return 0;
+}
+
+// distinct keys of vk (m x 32 bytes) not yet cached, in first-occurrence order; of[i] = the
+// cache index key i will have
+static int kc_collect(edc_ctx* ctx, size_t m, const uint8_t* vk, std::vector<uint32_t>& of,
+                      std::vector<uint32_t>& neww) {
   std::unordered_map<std::string, uint32_t> idx;
-  std::vector<uint32_t> of(m), words;
+  for (uint32_t c = 0; c < ctx->kc_m; ++c)
+    idx.emplace(std::string(reinterpret_cast<const char*>(&ctx->kc_words[8 * c]), 32), c);
+  of.resize(m);
   for (size_t i = 0; i < m; ++i) {
     auto it = idx.emplace(std::string(reinterpret_cast<const char*>(vk + 32 * i), 32), (uint32_t)idx.size());
     of[i] = it.first->second;
@@ -1566,48 +1653,43 @@ int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok
       if (idx.size() > KC_MAX_KEYS) { ctx->err = "key cache holds at most 65536 keys"; return EDC_ERR_ARG; }
       uint32_t w[8];
       memcpy(w, vk + 32 * i, 32);
-      words.insert(words.end(), w, w + 8);
+      neww.insert(neww.end(), w, w + 8);
     }
   }
-  const uint32_t u = (uint32_t)idx.size();
-  const uint32_t T = (uint32_t)next_pow2(2 * (size_t)(u < 8 ? 8 : u));
-  std::vector<uint32_t> table(T, KC_EMPTY);
-  for (uint32_t c = 0; c < u; ++c) {
-    uint32_t h = kc_hash(&words[8 * c]) & (T - 1);
-    while (table[h] != KC_EMPTY) h = (h + 1) & (T - 1);
-    table[h] = c;
-  }
-  uint32_t* ext = nullptr;
-  CK(dalloc(&ctx->kc_table, T));
-  CK(dalloc(&ctx->kc_keys, (size_t)u * 8));
-  CK(dalloc(&ctx->kc_ok, u));
-  CK(dalloc(&ctx->kc_comb, (size_t)u * COMB_ENTRIES * NIELS_WORDS));
+  return 0;
+}
+
+int64_t edc_keycache_load(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok) {
+  if (!ctx || (m && !vk)) return EDC_ERR_ARG;
+  int rc = edc_keycache_clear(ctx);
+  if (rc) return rc;
+  if (!m) return 0;
+  // distinct keys in first-occurrence order (the cache is keyed on raw bytes, like the batch's
+  // HashMap<VerificationKeyBytes, _>, src/batch.rs:114)
+  std::vector<uint32_t> of, words;
+  if ((rc = kc_collect(ctx, m, vk, of, words))) return rc;
+  if ((rc = kc_append(ctx, words))) return rc;
   CK(dalloc(&ctx->kc_reg, m));
-  CK(dalloc(&ext, (size_t)(u + 1) * EXT_WORDS));
-  hipStream_t st = ctx->st();
-  CK(hipMemcpyAsync(ctx->kc_reg, of.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(ctx->kc_table, table.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(ctx->kc_keys, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  launch_kc_decode(st, u, ctx->kc_keys, ext, ctx->kc_ok);
-  launch_kc_comb(st, u, ext, ctx->kc_comb);
-  if (!ctx->bcomb) {
-    CK(dalloc(&ctx->bcomb, (size_t)COMB_ENTRIES * NIELS_WORDS));
-    uint32_t* bext = ext + (size_t)u * EXT_WORDS;
-    launch_kc_basepoint(st, bext);
-    launch_kc_comb(st, 1, bext, ctx->bcomb);
-  }
-  CK(hipGetLastError());
-  std::vector<uint8_t> uok(u);
-  CK(hipMemcpyAsync(uok.data(), ctx->kc_ok, u, hipMemcpyDeviceToHost, st));
-  CK(hipStreamSynchronize(st));
-  (void)hipFree(ext);
-  ctx->kc_m = u;
-  ctx->last_uncached = 0;                    // try split coefficients with the new key set
-  ctx->kc_tmask = T - 1;
+  CK(hipMemcpy(ctx->kc_reg, of.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice));
   ctx->kc_reg_m = (uint32_t)m;
   if (ok)
-    for (size_t i = 0; i < m; ++i) ok[i] = uok[of[i]];
-  return u;
+    for (size_t i = 0; i < m; ++i) ok[i] = ctx->kc_okh[of[i]];
+  return ctx->kc_m;
+}
+
+int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok) {
+  if (!ctx || (m && !vk)) return EDC_ERR_ARG;
+  CK(hipSetDevice(ctx->device));
+  for (Slot& s : ctx->slot)
+    if (s.pending) { ctx->err = "key cache change with a batch in flight"; return EDC_ERR_ARG; }
+  int rc = sync_all(ctx);
+  if (rc) return rc;
+  std::vector<uint32_t> of, words;
+  if ((rc = kc_collect(ctx, m, vk, of, words))) return rc;
+  if ((rc = kc_append(ctx, words))) return rc;
+  if (ok)
+    for (size_t i = 0; i < m; ++i) ok[i] = ctx->kc_okh[of[i]];
+  return ctx->kc_m;
 }
 
 int edc_sign_device(edc_ctx* ctx, size_t n, const uint8_t* d_seeds, const uint32_t* d_seed_index,

@@ -35,15 +35,18 @@ struct KeyCacheView {
   uint32_t tmask;
   uint32_t m;
   const uint32_t* bcomb;   // COMB_ENTRIES records of B (built with the first cache)
+  uint32_t s0, s1;         // hash key (per-context secret: keys added from untrusted input cannot
+                           // be chosen to collide in the table)
 };
 
-__host__ __device__ inline uint32_t kc_hash(const uint32_t w[8]) {
-  uint32_t h = 0x2545F491u;
+__host__ __device__ inline uint32_t kc_hash(const uint32_t w[8], uint32_t s0, uint32_t s1) {
+  uint32_t h = 0x2545F491u ^ s0;
   for (int j = 0; j < 8; ++j) {
     h ^= w[j];
     h *= 0x9E3779B1u;
     h ^= h >> 15;
   }
+  h ^= s1;
   h *= 0x85EBCA77u;
   h ^= h >> 13;
   return h;
@@ -53,7 +56,7 @@ __host__ __device__ inline uint32_t kc_hash(const uint32_t w[8]) {
 // cache index of the raw key bytes w, or -1
 __device__ __forceinline__ int kc_lookup(const KeyCacheView& kc, const uint32_t w[8]) {
   if (!kc.table) return -1;
-  uint32_t h = kc_hash(w) & kc.tmask;
+  uint32_t h = kc_hash(w, kc.s0, kc.s1) & kc.tmask;
   for (uint32_t probe = 0; probe <= kc.tmask; ++probe) {
     const uint32_t c = kc.table[h];
     if (c == KC_EMPTY) return -1;

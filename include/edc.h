@@ -282,6 +282,19 @@ int edc_keycache_clear(edc_ctx* ctx);
 size_t edc_keycache_size(const edc_ctx* ctx);
 
 /*
+ * Per-object decoded key (reference src/verification_key.rs:106-114, :160-175: VerificationKey
+ * decodes A once at try_from and keeps minus_A for every later verify): adds the keys of vk (m x 32
+ * bytes) that are not cached yet to this context's cache WITHOUT replacing it. Cached keys keep
+ * their places, so the list last given to edc_keycache_load stays valid for
+ * edc_batch_submit_indexed (this call does not change that list). Every later batch or per-item
+ * call finds a key added here exactly as one loaded by edc_keycache_load. ok (nullable, m bytes)
+ * as edc_keycache_load. The table's hash is keyed by a per-context secret, so keys taken from
+ * untrusted input cannot be chosen to collide. Returns the number of distinct keys now cached or
+ * <0; refused while submitted batches are in flight.
+ */
+int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok);
+
+/*
  * SigningKey::from([u8;32]) + SigningKey::sign (reference src/signing_key.rs:118-150,
  * :186-205) -- test/benchmark data source. seed_index (nullable) maps item i to seed
  * seed_index[i] (shared validator keys); vk_out n*32, sig_out n*64.

@@ -70,31 +70,39 @@ def test_zip215_corpus_single_and_batch(engine, edc):
         code, check8 = engine.batch_verify([vk], [sig], [msg], z_seed=bytes([0x33]) * 32, want_check8=True)
         assert code == c["expect_batch1"] == 0
         assert check8 == bytes([1]) + bytes(31)
-    # the reference test body, through the mirrored API (tests/small_order.rs:88-104)
-    for vk, sig in list(zip(vks, sigs))[::13]:
-        single_ok = True
-        try:
-            edc.VerificationKey.try_from(vk, engine).verify(sig, msg)
-        except edc.Error:
-            single_ok = False
-        bv = edc.batch.Verifier(engine)
-        bv.queue((vk, sig, msg))
-        try:
-            bv.verify(bytes(32))
-            batch_ok = True
-        except edc.InvalidSignature:
-            batch_ok = False
-        assert single_ok == batch_ok
+    # the reference test body, through the mirrored API (tests/small_order.rs:88-104); try_from
+    # keeps each decoded key in the engine's cache, dropped again at the end
+    try:
+        for vk, sig in list(zip(vks, sigs))[::13]:
+            single_ok = True
+            try:
+                edc.VerificationKey.try_from(vk, engine).verify(sig, msg)
+            except edc.Error:
+                single_ok = False
+            bv = edc.batch.Verifier(engine)
+            bv.queue((vk, sig, msg))
+            try:
+                bv.verify(bytes(32))
+                batch_ok = True
+            except edc.InvalidSignature:
+                batch_ok = False
+            assert single_ok == batch_ok
+    finally:
+        engine.keycache_clear()
 
 
 def test_rfc8032_via_api(engine, edc):
-    for v in golden("rfc8032.json")["vectors"]:
-        sk, pk, sig, msg = (bytes.fromhex(v[k]) for k in ("sk", "pk", "sig", "msg"))
-        vk = edc.VerificationKey.try_from(pk, engine)
-        vk.verify(sig, msg)
-        key = edc.SigningKey(sk, engine)
-        assert key.sign(msg).to_bytes() == sig
-        assert key.verification_key_bytes().to_bytes() == pk
+    try:
+        for v in golden("rfc8032.json")["vectors"]:
+            sk, pk, sig, msg = (bytes.fromhex(v[k]) for k in ("sk", "pk", "sig", "msg"))
+            vk = edc.VerificationKey.try_from(pk, engine)
+            assert vk.cached
+            vk.verify(sig, msg)
+            key = edc.SigningKey(sk, engine)
+            assert key.sign(msg).to_bytes() == sig
+            assert key.verification_key_bytes().to_bytes() == pk
+    finally:
+        engine.keycache_clear()
 
 
 def test_reference_batch_tests_via_api(engine, edc):
