@@ -205,6 +205,9 @@ def main():
     ap.add_argument("--multi", type=int, default=1,
                     help="verify this many consecutive batches of --n signatures per launch sequence "
                          "(edc_batch_submit_multi_device; each keeps its own verdict and z range)")
+    ap.add_argument("--multi-exact", action="store_true",
+                    help="with --multi: every launch batch by batch (edc_set_multi_union(0)) instead of the "
+                         "default union first (one batch over all items, rerun batch by batch only on failure)")
     ap.add_argument("--prehashed", action="store_true",
                     help="time edc_batch_submit_prehashed_device: items carry their queue-time k (the reference's "
                          "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
@@ -250,8 +253,10 @@ def main():
     slots = max(1, 16 // sharing)
     nmb = max(1, args.multi)                       # batches per launch sequence
     if args.inflight <= 0:
-        if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh)
+        if nmb > 1 and args.multi_exact:   # batch by batch: 3 launches of >= 2^20 items (tools/sweep_multi.sh)
             args.inflight = 3 if n * nmb >= (1 << 19) else 4
+        elif nmb > 1:  # union first: each launch runs as one batch of n * nmb items
+            args.inflight = 6 if n * nmb >= (1 << 19) else 16
         else:
             args.inflight = 6 if n >= (1 << 19) else 16
     args.inflight = min(args.inflight, slots)
@@ -259,6 +264,8 @@ def main():
         args.warmup = max(args.warmup, args.inflight + 1)
     # the context rotates over exactly `inflight` slots, so only that many slot streams (hardware
     # queues) exist beside RCCL's own in a multi-rank run; a build with fewer slots keeps its count
+    if nmb > 1:
+        eng.set_multi_union(not args.multi_exact)
     if eng.lib.edc_set_slots(eng.ctx, args.inflight) < 0 and sharing > 1:
         raise RuntimeError("cannot split the GPU's slots between the ranks sharing it")
     t_gen = time.perf_counter()
@@ -452,6 +459,7 @@ def main():
                        "sigs_per_gpu": n, "validators": args.keys or "distinct", "msg_len": args.msg_len,
                        "inflight": args.inflight, "keycache": bool(args.keycache and args.keys > 0),
                        "prehashed": bool(args.prehashed), "batches_per_launch": nmb,
+                       "multi_union_first": bool(nmb > 1 and not args.multi_exact),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),

@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_keycache_add",
+    "edc_keycache_add", "edc_set_multi_union", "edc_multi_union_stats",
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
@@ -185,6 +185,10 @@ def load_library(path=None):
         lib.edc_vk_validate.argtypes = [c_vp, c_sz, c_u8p, c_vp]
         lib.edc_keycache_load.restype = ctypes.c_int64
         lib.edc_keycache_load.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+        lib.edc_set_multi_union.restype = ctypes.c_int
+        lib.edc_set_multi_union.argtypes = [c_vp, ctypes.c_int]
+        lib.edc_multi_union_stats.restype = ctypes.c_int
+        lib.edc_multi_union_stats.argtypes = [c_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         lib.edc_keycache_add.restype = ctypes.c_int64
         lib.edc_keycache_add.argtypes = [c_vp, c_sz, c_u8p, c_vp]
         lib.edc_keycache_clear.argtypes = [c_vp]
@@ -344,17 +348,28 @@ class Engine:
         self._check(t)
         return t
 
-    def batch_wait_multi(self, ticket, nb):
-        """(code, [verdict per batch], [check8 per batch], [partial per batch], [bad per batch])."""
+    def batch_wait_multi(self, ticket, nb, want_partials=False):
+        """(code, [verdict per batch], [check8 per batch], [partial per batch] or None, [bad per batch]).
+        Asking for the partials makes a union-first launch run batch by batch (edc_set_multi_union)."""
         v = (ctypes.c_int * nb)()
         bad = (ctypes.c_int * nb)()
         c8 = ctypes.create_string_buffer(32 * nb)
-        parts = ctypes.create_string_buffer(128 * nb)
+        parts = ctypes.create_string_buffer(128 * nb) if want_partials else None
         with self._lock:
             rc = self.lib.edc_batch_wait_multi(self.ctx, ticket, nb, v, c8, parts, bad)
         self._check(rc)
         return (rc, list(v), [c8.raw[32 * g:32 * g + 32] for g in range(nb)],
-                [parts.raw[128 * g:128 * g + 128] for g in range(nb)], list(bad))
+                [parts.raw[128 * g:128 * g + 128] for g in range(nb)] if want_partials else None, list(bad))
+
+    def set_multi_union(self, on):
+        """Multi-batch launches verify the union of their batches first (default on)."""
+        self._check(self.lib.edc_set_multi_union(self.ctx, 1 if on else 0))
+
+    def multi_union_stats(self):
+        """(union-first launches that passed, launches rerun batch by batch) on this context."""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._check(self.lib.edc_multi_union_stats(self.ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def batch_wait(self, ticket, want_check8=False):
         """Verdict of a submitted batch: (code, check8 or None); the ticket's host buffers are released."""

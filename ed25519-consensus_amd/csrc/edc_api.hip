@@ -82,6 +82,17 @@ struct Slot {
   uint8_t* mb_bad = nullptr;
   size_t mb_cap_acc = 0, mb_cap_terms = 0;
   uint32_t nmulti = 0;
+  // union-first multi launch (edc_set_multi_union): the launch ran as ONE batch over all nb * n_per
+  // items; its arguments are kept (device inputs are borrowed until the wait) to rerun it batch by
+  // batch when that union fails
+  bool mu_union = false;
+  size_t mu_nper = 0;
+  const uint8_t *mu_vk = nullptr, *mu_sig = nullptr, *mu_msg = nullptr;
+  const uint64_t* mu_off = nullptr;
+  const uint32_t* mu_k = nullptr;
+  uint8_t mu_seed[32] = {};
+  uint64_t mu_zbase = 0;
+  int mu_compress = 0;
   hipEvent_t ev[PH_N + 1] = {};
   // EDC_DUAL_STREAM builds: the decode runs on a second stream beside SHA-512 / coefficients /
   // binning (joined before the accumulation)
@@ -159,6 +170,8 @@ struct edc_ctx {
   // key_split 0 = auto, 1 = never; last_uncached = keys the last batch did not find in the cache
   int key_split = 0;
   uint32_t last_uncached = 0;
+  int multi_union = 1;                  // edc_set_multi_union
+  uint64_t mu_hits = 0, mu_reruns = 0;  // union-first launches that passed / were rerun per batch
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
     if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, 0, 0};
@@ -727,21 +740,28 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
 // fallback's range machinery (k_coef range mode, listed key / B terms) with the key count left
 // on the device: per-(batch, key) sums sit at b * kstride + key and the term layout is resolved
 // from the key grouping by the binning kernels (MsmTerms::dyn).
-static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
-                         const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_k, const uint8_t* z_seed,
-                         uint64_t z_base, int want_compress) {
+static int multi_args(edc_ctx* ctx, uint32_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
+                      const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_k) {
   if (nb < 1 || nb > kMultiMax || n_per == 0 || n_per % COEF_CHUNK) {
     ctx->err = "multi-batch: 1..16 batches of a multiple of 2048 items each";
     return EDC_ERR_ARG;
   }
-  const size_t N = (size_t)nb * n_per;
-  if (N >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
+  if ((size_t)nb * n_per >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   if (!aligned16(d_vk) || !aligned16(d_sig) || (d_k && !aligned16(d_k))) {
     ctx->err = "device vk / sig / k arrays must be 16-byte aligned";
     return EDC_ERR_ARG;
   }
   if (!d_k && (!d_msg || !d_off)) { ctx->err = "null msg"; return EDC_ERR_ARG; }
-  int rc = ensure_slot(ctx, s, N);
+  return 0;
+}
+
+static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
+                         const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_k, const uint8_t* z_seed,
+                         uint64_t z_base, int want_compress) {
+  int rc = multi_args(ctx, nb, n_per, d_vk, d_sig, d_msg, d_off, d_k);
+  if (rc) return rc;
+  const size_t N = (size_t)nb * n_per;
+  rc = ensure_slot(ctx, s, N);
   if (rc) return rc;
   const bool per_sig = choose_per_sig(ctx, N);
   const uint32_t kstride = (uint32_t)(N < kMultiKeys ? N : kMultiKeys);
@@ -827,6 +847,50 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
 static int finish_multi(edc_ctx* ctx, Slot& s, size_t nb, int* verdicts, uint8_t* check8, uint8_t* partials, int* bad) {
   if (!s.pending || !s.nmulti) { ctx->err = "no multi-batch pending in this slot"; return EDC_ERR_ARG; }
   if (nb != s.nmulti) { ctx->err = "multi-batch count differs from the submission"; return EDC_ERR_ARG; }
+  if (s.mu_union) {
+    // The launch ran as one batch over all nb * n_per items (z at the same global indices). Its
+    // equation is the sum of the nb batches' equations, so when it holds every batch holds (with
+    // the probability batch verification itself gives: src/batch.rs:149-217) and each batch's
+    // [8]*check is the identity. Otherwise, or when the caller wants the per-batch partials, the
+    // launch is rerun range by range on the same slot (the inputs are still borrowed).
+    s.mu_union = false;
+    CK(hipStreamSynchronize(s.st));
+    const int* u = reinterpret_cast<const int*>(s.h_out);
+    if (u[45]) {
+      s.pending = false;
+      s.nmulti = 0;
+      ctx->err = "prehashed k is not a canonical scalar (must be < l, as Scalar::from_hash returns)";
+      return EDC_ERR_ARG;
+    }
+    if (!u[0] && !u[1] && !partials) {
+      s.pending = false;
+      s.nmulti = 0;
+      if (s.per_sig) {
+        ctx->ungrouped_run++;
+      } else {
+        ctx->ungrouped_run = 0;
+        ctx->have_key_ratio = true;
+        ctx->last_key_ratio = (double)u[2] / (double)s.n_batch;
+      }
+      if (ctx->kc_m) ctx->last_uncached = (uint32_t)u[44];
+      ctx->mu_hits++;
+      for (size_t g = 0; g < nb; ++g) {
+        if (verdicts) verdicts[g] = EDC_OK;
+        if (bad) bad[g] = 0;
+        if (check8) {
+          memset(check8 + 32 * g, 0, 32);
+          check8[32 * g] = 1;                         // compressed identity
+        }
+      }
+      return EDC_OK;
+    }
+    ctx->mu_reruns++;
+    s.pending = false;
+    s.nmulti = 0;
+    int rc = enqueue_multi(ctx, s, (uint32_t)nb, s.mu_nper, s.mu_vk, s.mu_sig, s.mu_msg, s.mu_off, s.mu_k, s.mu_seed,
+                           s.mu_zbase, s.mu_compress || check8 != nullptr);
+    if (rc) return rc;
+  }
   s.pending = false;
   s.nmulti = 0;
   CK(hipStreamSynchronize(s.st));
@@ -1101,9 +1165,29 @@ int64_t edc_batch_submit_multi_device(edc_ctx* ctx, size_t nb, size_t n_per, con
   const int64_t ticket = ctx->next_ticket;
   Slot& s = ctx->slot[ticket % ctx->nslots];
   if (s.pending) { ctx->err = "all slots in flight: wait for the oldest ticket first"; return EDC_ERR_ARG; }
-  int rc = enqueue_multi(ctx, s, (uint32_t)(nb <= kMultiMax ? nb : 0), n_per, d_vk, d_sig, d_msg, d_msg_off,
-                         reinterpret_cast<const uint32_t*>(d_k), z_seed, z_base, want_check8 != 0);
-  if (rc) return rc;
+  const uint32_t nbv = (uint32_t)(nb <= kMultiMax ? nb : 0);
+  const uint32_t* dk = reinterpret_cast<const uint32_t*>(d_k);
+  int rc;
+  if (ctx->multi_union) {        // one batch over all items first (finish_multi)
+    rc = multi_args(ctx, nbv, n_per, d_vk, d_sig, d_msg, d_msg_off, dk);
+    if (!rc) rc = enqueue_batch(ctx, s, (size_t)nbv * n_per, d_vk, d_sig, d_msg, d_msg_off, z_seed, z_base, nullptr, 0, dk);
+    if (rc) return rc;
+    s.nmulti = nbv;
+    s.mu_union = true;
+    s.mu_nper = n_per;
+    s.mu_vk = d_vk;
+    s.mu_sig = d_sig;
+    s.mu_msg = d_msg;
+    s.mu_off = d_msg_off;
+    s.mu_k = dk;
+    memcpy(s.mu_seed, z_seed, 32);
+    s.mu_zbase = z_base;
+    s.mu_compress = want_check8 != 0;
+  } else {
+    rc = enqueue_multi(ctx, s, nbv, n_per, d_vk, d_sig, d_msg, d_msg_off, dk, z_seed, z_base, want_check8 != 0);
+    if (rc) return rc;
+    s.mu_union = false;
+  }
   s.ticket = ticket;
   ctx->next_ticket++;
   return ticket;
@@ -1116,6 +1200,19 @@ int edc_batch_wait_multi(edc_ctx* ctx, int64_t ticket, size_t nb, int* verdicts,
   Slot& s = ctx->slot[ticket % ctx->nslots];
   if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
   return finish_multi(ctx, s, nb, verdicts, check8, partials, bad);
+}
+
+int edc_set_multi_union(edc_ctx* ctx, int on) {
+  if (!ctx) return EDC_ERR_ARG;
+  ctx->multi_union = on ? 1 : 0;
+  return 0;
+}
+
+int edc_multi_union_stats(const edc_ctx* ctx, uint64_t* passed, uint64_t* rerun) {
+  if (!ctx) return EDC_ERR_ARG;
+  if (passed) *passed = ctx->mu_hits;
+  if (rerun) *rerun = ctx->mu_reruns;
+  return 0;
 }
 
 int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,

@@ -108,14 +108,25 @@ int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t par
  * of batch b alone at z_base + b n_per. Every per-item kernel runs once over all nb n_per items
  * and the MSM is range-tagged (one range per batch), so small batches fill the GPU like one
  * large batch. Waited with edc_batch_wait_multi (same ticket rules as edc_batch_submit_device):
- * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32, needs want_check8),
- * partials (nb x 128) and bad flags (nb); returns EDC_INVALID_SIGNATURE if any batch failed.
+ * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32), partials (nb x 128)
+ * and bad flags (nb); returns EDC_INVALID_SIGNATURE if any batch failed.
+ *
+ * Union first (default; edc_set_multi_union): the launch runs as ONE batch over all nb n_per items
+ * (same z). Its equation is the sum of the batches' equations, so when it holds every batch holds
+ * -- with the probability batch verification itself gives, as Verifier::verify accepting a batch
+ * accepts each of its items -- and every batch reports EDC_OK, bad 0 and the identity as check8.
+ * When it fails (or partials are asked for at the wait), the wait reruns the launch batch by batch
+ * as above before returning, so failing batches get exactly their own verdict, bad flag and
+ * check8. edc_set_multi_union(ctx, 0) always runs batch by batch; edc_multi_union_stats counts the
+ * union launches that passed and those rerun.
  */
 int64_t edc_batch_submit_multi_device(edc_ctx* ctx, size_t nb, size_t n_per, const uint8_t* d_vk, const uint8_t* d_sig,
                                       const uint8_t* d_msg, const uint64_t* d_msg_off, const uint8_t* d_k,
                                       const uint8_t z_seed[32], uint64_t z_base, int want_check8);
 int edc_batch_wait_multi(edc_ctx* ctx, int64_t ticket, size_t nb, int* verdicts, uint8_t* check8, uint8_t* partials,
                          int* bad);
+int edc_set_multi_union(edc_ctx* ctx, int on);
+int edc_multi_union_stats(const edc_ctx* ctx, uint64_t* passed, uint64_t* rerun);
 
 /*
  * Host-buffer form of edc_batch_submit_device (replaces src/batch.rs:149 `Verifier::verify` for a

@@ -5,7 +5,10 @@ that batch alone gives: verdict, bad flag, compressed [8]*check (reference src/b
 once per batch); failing batches are also pinned to the C oracle. Covered: grouped keys (votes),
 distinct keys (one key term per signature, by the host's choice and by the device's key-count
 cap), the forced grouping overflow, undecodable R / non-canonical s / undecodable key in one
-batch only, prehashed k, and full size (8 x 2^17 votes = 2^20)."""
+batch only, prehashed k, and full size (8 x 2^17 votes = 2^20). Each comparison runs in three
+modes: union first (the default: the launch is verified as one batch and rerun batch by batch only
+when that fails), batch by batch (edc_set_multi_union(0)), and union first with the per-batch
+partials asked for (which reruns it batch by batch)."""
 import ctypes
 import os
 import random
@@ -73,12 +76,21 @@ def _single(engine, d, b, n_per, offs, zseed, z_base, torch):
     return code, c8.raw, part.raw, bad.value
 
 
-def _multi(engine, d, nb, n_per, zseed, z_base, d_k=None):
+def _multi(engine, d, nb, n_per, zseed, z_base, d_k=None, want_partials=False):
     t = engine.batch_submit_multi_device(nb, n_per, d["vk"].data_ptr(), d["sig"].data_ptr(),
                                          d["msg"].data_ptr() if d_k is None else None,
                                          d["off"].data_ptr() if d_k is None else None, zseed, z_base,
                                          d_k=d_k, want_check8=True)
-    return engine.batch_wait_multi(t, nb)
+    return engine.batch_wait_multi(t, nb, want_partials=want_partials)
+
+
+@pytest.fixture(params=["union", "exact", "partials"])
+def mode(request, engine):
+    """union: union-first launches (default); exact: edc_set_multi_union(0); partials: union-first
+    with the per-batch partials asked for at the wait (which reruns the launch batch by batch)."""
+    engine.set_multi_union(request.param != "exact")
+    yield request.param
+    engine.set_multi_union(True)
 
 
 def _check_against_single(engine, torch, d, nb, n_per, offs, zseed, z_base, res):
@@ -88,14 +100,14 @@ def _check_against_single(engine, torch, d, nb, n_per, offs, zseed, z_base, res)
         assert verdicts[b] == sc, b
         assert bads[b] == sbad, b
         assert c8s[b] == sc8, b
-        if not sbad:       # partials are projective: compare [8]*P of the two
+        if not sbad and parts is not None:       # partials are projective: compare [8]*P of the two
             assert engine.combine_partials([parts[b]], 0) == engine.combine_partials([spart], 0), b
     assert code == (1 if any(verdicts) else 0)
 
 
 @pytest.mark.parametrize("keys,grouping", [(20, 0), (0, 2), (0, 1), (20, 3)],
                          ids=["votes", "distinct_per_sig", "distinct_grouped_over_cap", "forced_overflow"])
-def test_multi_equals_single_batches(engine, keys, grouping):
+def test_multi_equals_single_batches(engine, mode, keys, grouping):
     torch = pytest.importorskip("torch")
     nb, n_per = 4, 2048 if grouping != 1 else 4096          # 16,384 distinct keys > the 4,096 cap
     spoil = [(1 * n_per + 77, "msg"), (2 * n_per + 5, "R"), (3 * n_per + 1000, "s")]
@@ -104,7 +116,7 @@ def test_multi_equals_single_batches(engine, keys, grouping):
     try:
         for z_base in (0, 12345):
             zseed = bytes([0x4D + z_base % 7]) * 32
-            res = _multi(engine, d, nb, n_per, zseed, z_base)
+            res = _multi(engine, d, nb, n_per, zseed, z_base, want_partials=mode == "partials")
             assert res[1] == [0, 1, 1, 1]
             assert res[4] == [0, 0, 1, 1]
             assert res[2][0] == IDENTITY
@@ -130,14 +142,46 @@ def test_multi_failing_batch_vs_oracle(engine):
     assert (oc_code, oc_c8) == (1, c8s[1])
 
 
-def test_multi_undecodable_key_in_one_batch(engine):
+def test_multi_undecodable_key_in_one_batch(engine, mode):
     torch = pytest.importorskip("torch")
     nb, n_per = 2, 2048
     vks, sigs, msgs, offs, d = _make(engine, torch, nb, n_per, 10, seed=9, spoil=[(n_per + 3, "A")])
     zseed = bytes([0x19]) * 32
-    res = _multi(engine, d, nb, n_per, zseed, 0)
+    res = _multi(engine, d, nb, n_per, zseed, 0, want_partials=mode == "partials")
     assert res[1] == [0, 1] and res[4] == [0, 1]
     _check_against_single(engine, torch, d, nb, n_per, offs, zseed, 0, res)
+
+
+def test_multi_union_first_counts(engine):
+    """A valid launch passes as one union (no rerun, identity check8 for every batch); a launch
+    with one failing batch is rerun batch by batch and reports that batch alone; asking for the
+    partials reruns a valid launch too; with the union off nothing is counted."""
+    torch = pytest.importorskip("torch")
+    nb, n_per = 4, 2048
+    vks, sigs, msgs, offs, d = _make(engine, torch, nb, n_per, 24, seed=77)
+    zseed = bytes([0x5C]) * 32
+    engine.set_multi_union(True)
+    h0, r0 = engine.multi_union_stats()
+    res = _multi(engine, d, nb, n_per, zseed, 0)
+    assert res[0] == 0 and res[1] == [0] * nb and res[2] == [IDENTITY] * nb and res[4] == [0] * nb
+    assert engine.multi_union_stats() == (h0 + 1, r0)
+    _check_against_single(engine, torch, d, nb, n_per, offs, zseed, 0, res)
+    res = _multi(engine, d, nb, n_per, zseed, 0, want_partials=True)
+    assert engine.multi_union_stats() == (h0 + 1, r0 + 1)
+    _check_against_single(engine, torch, d, nb, n_per, offs, zseed, 0, res)
+    d["sig"][64 * (2 * n_per + 9) + 40] ^= 0x10
+    torch.cuda.synchronize()
+    res = _multi(engine, d, nb, n_per, zseed, 0)
+    assert res[1] == [0, 0, 1, 0] and res[2][2] != IDENTITY
+    assert engine.multi_union_stats() == (h0 + 1, r0 + 2)
+    _check_against_single(engine, torch, d, nb, n_per, offs, zseed, 0, res)
+    engine.set_multi_union(False)
+    try:
+        res = _multi(engine, d, nb, n_per, zseed, 0)
+        assert res[1] == [0, 0, 1, 0]
+        assert engine.multi_union_stats() == (h0 + 1, r0 + 2)
+    finally:
+        engine.set_multi_union(True)
 
 
 def test_multi_prehashed(engine):

@@ -21,7 +21,8 @@
 #                    AB_CONFIGS (default "c3 n17 c2 c5"), AB_REPS rounds (default 2)
 #   bench=<args>     one bench.py run with these arguments (commas for spaces)
 #   pre              configs[2] with prehashed items (edc_batch_submit_prehashed_device)
-#   m17 | m16        8 consecutive 2^17 vote shards / configs[1] batches per launch (--multi 8)
+#   m17 | m16        8 consecutive 2^17 vote shards / configs[1] batches per launch (--multi 8, union first)
+#   m17x | m16x      the same batch by batch (--multi-exact)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -70,6 +71,8 @@ for step in "$@"; do
     pre) bench_step pre --prehashed --steps 40 --warmup 5 --no-cpu-baseline ;;
     m17) bench_step m17 --n 131072 --multi 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
     m16) bench_step m16 --config c2 --multi 8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    m17x) bench_step m17x --n 131072 --multi 8 --multi-exact --steps 20 --warmup 5 --no-cpu-baseline ;;
+    m16x) bench_step m16x --config c2 --multi 8 --multi-exact --steps 20 --warmup 5 --no-cpu-baseline ;;
     fallback) run fallback 300 python3 -u tools/fallback_bench.py ;;
     host) run host 300 python3 -u tools/host_bench.py ;;
     small) run small 300 python3 -u tools/smallbatch_bench.py ;;
