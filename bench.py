@@ -254,7 +254,7 @@ def main():
     nmb = max(1, args.multi)                       # batches per launch sequence
     if args.inflight <= 0:
         if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh;
-            # union first measured 6.38e8 at 3 and 5.55e8 at 6 at 8 x 2^17, profiles/r04/r04w_summary.log)
+            # union first measured 6.38e8 at 3 and 5.55e8 at 6 at 8 x 2^17, profiles/r04/r04w_union_inflight6_summary.log)
             args.inflight = 3 if n * nmb >= (1 << 19) else 4
         else:
             args.inflight = 6 if n >= (1 << 19) else 16
