@@ -103,9 +103,9 @@ int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t par
  * nb (1..16) batches of n_per items each (n_per a multiple of 2048), back to back in device
  * memory -- batch b is items [b n_per, (b+1) n_per) of d_vk / d_sig and of the message arena's
  * nb n_per + 1 offsets (or of d_k: nb n_per prehashed challenges, messages unused, d_msg /
- * d_msg_off may be NULL). Batch b's z are drawn at global indices z_base + b n_per + i, so its
- * verdict, bad flag, check8 and partial equal edc_batch_verify_device / edc_batch_partial_device
- * of batch b alone at z_base + b n_per. Every per-item kernel runs once over all nb n_per items
+ * d_msg_off may be NULL). Batch b's z are drawn at global indices z_base + b n_per + i, so batch
+ * by batch its verdict, bad flag, check8 and partial equal edc_batch_verify_device /
+ * edc_batch_partial_device of batch b alone at z_base + b n_per (see "Union first" below). Every per-item kernel runs once over all nb n_per items
  * and the MSM is range-tagged (one range per batch), so small batches fill the GPU like one
  * large batch. Waited with edc_batch_wait_multi (same ticket rules as edc_batch_submit_device):
  * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32), partials (nb x 128)
