@@ -423,6 +423,9 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
 #ifndef EDC_ACC_OCC
 #define EDC_ACC_OCC 4
 #endif
+#ifndef EDC_ACC_PROBE
+#define EDC_ACC_PROBE 0   // measurement knob: 1 = no row gathers after the first round, 2 = no LDS row reads either
+#endif
 __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32_t* __restrict__ counts,
                                                                    const uint32_t* __restrict__ offsets,
                                                                    const uint32_t* __restrict__ sorted,
@@ -492,6 +495,10 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
   uint32_t e = lo < hi ? sorted[off + lo] : 0u;
   uint32_t e_next = lo + 1 < hi ? sorted[off + lo + 1] : e;
   gather_rows(e & 0x7FFFFFFFu);
+#if EDC_ACC_PROBE >= 2
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  const ge_niels q0 = ld_row_lds(wrows + lane * ROW_WORDS);
+#endif
   for (uint32_t j = 0; j < rounds; ++j) {
     const uint32_t pos = lo + j;
     if (pos < hi && pos == cend) {                 // the running bucket ended: flush it
@@ -502,9 +509,15 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
       cend = lend[cb];
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): round j's rows are in LDS
+#if EDC_ACC_PROBE >= 2                             // measurement builds only (wrong results)
+    ge_niels q = q0;
+#else
     ge_niels q = ld_row_lds(wrows + lane * ROW_WORDS);
+#endif
     __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0): row in VGPRs before the refill
+#if EDC_ACC_PROBE == 0
     if (j + 1 < rounds) gather_rows(e_next & 0x7FFFFFFFu);   // lanes past their range re-read a row
+#endif
     const uint32_t e_cur = e;
     e = e_next;
     if (pos + 2 < hi) e_next = sorted[off + pos + 2];
