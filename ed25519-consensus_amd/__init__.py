@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "edc_find_invalid_device", "edc_verify_prehashed_each", "edc_challenge", "edc_decompress", "edc_sign",
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
-    "edc_keycache_add", "edc_set_multi_union", "edc_multi_union_stats",
+    "edc_keycache_add", "edc_set_multi_union", "edc_multi_union_stats", "edc_batch_submit_prehashed_indexed",
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
@@ -185,12 +185,17 @@ def load_library(path=None):
         lib.edc_vk_validate.argtypes = [c_vp, c_sz, c_u8p, c_vp]
         lib.edc_keycache_load.restype = ctypes.c_int64
         lib.edc_keycache_load.argtypes = [c_vp, c_sz, c_u8p, c_vp]
-        lib.edc_set_multi_union.restype = ctypes.c_int
-        lib.edc_set_multi_union.argtypes = [c_vp, ctypes.c_int]
-        lib.edc_multi_union_stats.restype = ctypes.c_int
-        lib.edc_multi_union_stats.argtypes = [c_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
-        lib.edc_keycache_add.restype = ctypes.c_int64
-        lib.edc_keycache_add.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+        if hasattr(lib, "edc_keycache_add"):                 # absent from older A/B builds (tools/)
+            lib.edc_set_multi_union.restype = ctypes.c_int
+            lib.edc_set_multi_union.argtypes = [c_vp, ctypes.c_int]
+            lib.edc_multi_union_stats.restype = ctypes.c_int
+            lib.edc_multi_union_stats.argtypes = [c_vp, ctypes.POINTER(ctypes.c_uint64),
+                                                  ctypes.POINTER(ctypes.c_uint64)]
+            lib.edc_keycache_add.restype = ctypes.c_int64
+            lib.edc_keycache_add.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+            lib.edc_batch_submit_prehashed_indexed.restype = ctypes.c_int64
+            lib.edc_batch_submit_prehashed_indexed.argtypes = [c_vp, c_sz, ctypes.POINTER(ctypes.c_uint32), c_u8p,
+                                                               c_u8p, c_u8p, ctypes.c_uint64, ctypes.c_int]
         lib.edc_keycache_clear.argtypes = [c_vp]
         lib.edc_keycache_size.restype = c_sz
         lib.edc_keycache_size.argtypes = [c_vp]
@@ -292,6 +297,20 @@ class Engine:
         with self._lock:
             t = self.lib.edc_batch_submit_prehashed(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], z_base,
                                                     1 if want_check8 else 0)
+            if t < 0:
+                self._check(t)
+            self._host_inflight[t] = bufs
+        return t
+
+    def batch_submit_prehashed_indexed(self, key_idx, sigs, ks, z_seed, z_base=0, want_check8=False):
+        """edc_batch_submit_prehashed with keys given as positions in the last keycache_load list
+        (100 bytes per item over PCIe)."""
+        n = len(sigs)
+        idx = (ctypes.c_uint32 * max(n, 1))(*key_idx)
+        bufs = (idx, b"".join(sigs) or b"\0", b"".join(ks) or b"\0", bytes(z_seed))
+        with self._lock:
+            t = self.lib.edc_batch_submit_prehashed_indexed(self.ctx, n, bufs[0], bufs[1], bufs[2], bufs[3], z_base,
+                                                            1 if want_check8 else 0)
             if t < 0:
                 self._check(t)
             self._host_inflight[t] = bufs

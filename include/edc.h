@@ -241,6 +241,15 @@ int64_t edc_batch_submit_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, co
 int64_t edc_batch_submit_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                                           const uint8_t* d_k, const uint8_t z_seed[32], uint64_t z_base,
                                           const uint8_t* d_z, int want_check8);
+/*
+ * edc_batch_submit_prehashed with the keys given as positions in the list last given to
+ * edc_keycache_load (as edc_batch_submit_indexed): 4 + 64 + 32 = 100 bytes per item over PCIe, for
+ * a node whose votes come from its registered validator set. Verdicts and check8 equal
+ * edc_batch_submit_prehashed with those keys. An index outside the list -> EDC_ERR_ARG.
+ */
+int64_t edc_batch_submit_prehashed_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx, const uint8_t* sig,
+                                           const uint8_t* k, const uint8_t z_seed[32], uint64_t z_base,
+                                           int want_check8);
 int edc_batch_verify_prehashed_fallback(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
                                         const uint8_t* k, const uint8_t z_seed[32], uint8_t* verdicts,
                                         int* n_invalid, uint8_t check8[32]);

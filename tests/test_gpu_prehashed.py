@@ -251,3 +251,21 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
                                       d_off.data_ptr(), d_v.data_ptr()) == 0
     single = bytes(d_v.cpu().tolist())
     assert v.raw == single and cnt.value == sum(1 for x in single if x)
+
+
+@pytest.mark.parametrize("b", [b for b in BATCHES if b["items"]], ids=lambda b: b["name"])
+def test_golden_prehashed_indexed(engine, edc, b):
+    """edc_batch_submit_prehashed_indexed: keys as positions in the registered list (100 B per item
+    over PCIe) give the fixture's verdict and check8."""
+    vks, sigs, _, ks = _items(b)
+    zseed = bytes.fromhex(b["z_seed"])
+    distinct = list(dict.fromkeys(vks))
+    pos = {v: i for i, v in enumerate(distinct)}
+    try:
+        engine.keycache_load(distinct)
+        t = engine.batch_submit_prehashed_indexed([pos[v] for v in vks], sigs, ks, zseed, want_check8=True)
+        _check(b, *engine.batch_wait(t, want_check8=True))
+        with pytest.raises(edc.EngineError, match="registered"):
+            engine.batch_submit_prehashed_indexed([len(distinct)] + [0] * (len(vks) - 1), sigs, ks, zseed)
+    finally:
+        engine.keycache_clear()
