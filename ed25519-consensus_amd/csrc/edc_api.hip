@@ -1698,12 +1698,12 @@ static int kc_append(edc_ctx* ctx, const std::vector<uint32_t>& neww) {
     if (cap > KC_MAX_KEYS) cap = KC_MAX_KEYS;
     uint32_t *keys = nullptr, *comb = nullptr;
     uint8_t* okd = nullptr;
-    CK(dalloc(&keys, (size_t)cap * 8));
-    CK(dalloc(&okd, cap));
-    if (hipMalloc(&comb, (size_t)cap * comb_words * sizeof(uint32_t)) != hipSuccess) {
+    if (dalloc(&keys, (size_t)cap * 8) != hipSuccess || dalloc(&okd, cap) != hipSuccess ||
+        dalloc(&comb, (size_t)cap * comb_words) != hipSuccess) {
       (void)hipGetLastError();
-      (void)hipFree(keys);
-      (void)hipFree(okd);
+      if (keys) (void)hipFree(keys);
+      if (okd) (void)hipFree(okd);
+      if (comb) (void)hipFree(comb);
       ctx->err = "key cache: out of device memory";
       return EDC_ERR_NOMEM;
     }
