@@ -108,8 +108,9 @@ int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t par
  * edc_batch_partial_device of batch b alone at z_base + b n_per (see "Union first" below). Every per-item kernel runs once over all nb n_per items
  * and the MSM is range-tagged (one range per batch), so small batches fill the GPU like one
  * large batch. Waited with edc_batch_wait_multi (same ticket rules as edc_batch_submit_device):
- * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32), partials (nb x 128)
- * and bad flags (nb); returns EDC_INVALID_SIGNATURE if any batch failed.
+ * verdicts[b] (EDC_OK / EDC_INVALID_SIGNATURE), optional check8 (nb x 32; a launch run batch by
+ * batch from the start, edc_set_multi_union(ctx, 0), computes it only with want_check8),
+ * partials (nb x 128) and bad flags (nb); returns EDC_INVALID_SIGNATURE if any batch failed.
  *
  * Union first (default; edc_set_multi_union): the launch runs as ONE batch over all nb n_per items
  * (same z). Its equation is the sum of the batches' equations, so when it holds every batch holds
