@@ -44,7 +44,10 @@ constexpr int kSlots = EDC_SLOTS;  // batches that can be in flight per context
 #ifndef EDC_DUAL_STREAM
 #define EDC_DUAL_STREAM 2   // slot 0 (synchronous calls) decodes on a second stream; see init_slot
 #endif
-constexpr size_t kQuadVerifyMax = 1u << 16;   // per-item lists up to this size use the quad kernel
+#ifndef EDC_QUAD_VERIFY_MAX
+#define EDC_QUAD_VERIFY_MAX (1u << 14)   // one lane per item beats a quad from ~32k items (r04ad)
+#endif
+constexpr size_t kQuadVerifyMax = EDC_QUAD_VERIFY_MAX;   // per-item lists up to this size use the quad kernel
 constexpr uint32_t kMultiMax = 16;            // batches per edc_batch_submit_multi_device launch
 constexpr uint32_t kMultiKeys = 4096;         // distinct keys with per-(batch, key) sums; more -> per signature
 
@@ -152,8 +155,8 @@ struct edc_ctx {
   size_t fb_cap_idx = 0;
   uint8_t* fb_g = nullptr;       // their gathered vk | sig | k (fb_cap_g items each)
   size_t fb_cap_g = 0;
-  uint32_t fb_ranges = 32;      // target range count of the grouped fallback
-  int fb_bits = 10;             // its window width
+  uint32_t fb_ranges = 128;     // target range count of the grouped fallback (sweep: profiles/r04/r04ad_fb_sweep.log)
+  int fb_bits = 9;              // its window width
   // persistent validator-key cache (keycache.h), replaced by each edc_keycache_load, grown by
   // edc_keycache_add (device arrays hold kc_cap keys; the host keeps the key words and ok bytes
   // to rebuild the hash table and answer duplicates)
@@ -1325,7 +1328,7 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
   return 0;
 }
 
-// ---- grouped fallback: one MSM pass over ~32 contiguous ranges (edc_set_fallback_shape) ----
+// ---- grouped fallback: one MSM pass over ~128 contiguous ranges (edc_set_fallback_shape) ----
 static int ensure_fb(edc_ctx* ctx, size_t terms, size_t ranges) {
   if (terms > ctx->fb_cap_terms || !ctx->fb_xpt) {
     CK(hipStreamSynchronize(ctx->st()));
@@ -1397,7 +1400,7 @@ static int verify_listed(edc_ctx* ctx, Slot& s, const std::vector<uint32_t>& idx
 
 // After a failed batch on slot s (its k, decoded points, key grouping and per-item failure bits
 // still in place): the batch equation restricted to ~fb_ranges (default 32) contiguous ranges in
-// ONE MSM pass (range-tagged bins, fb_bits = 10-bit windows by default), [8]P_g == 0 per range; ranges whose check fails or that
+// ONE MSM pass (range-tagged bins, fb_bits = 9-bit windows by default), [8]P_g == 0 per range; ranges whose check fails or that
 // hold an item with an undecodable R / key or a non-canonical s are verified item by item.
 // Items of passing ranges are valid (ZIP215: batch == single, with a fresh secret z: see
 // include/edc.h). verdicts (host, n bytes) receive Item::verify_single's code for every item.

@@ -183,7 +183,7 @@ int edc_verify_each_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const ui
 /*
  * Grouped fallback after a failed batch (the caller-driven Item::verify_single loop of
  * reference tests/batch.rs:37-43, src/batch.rs:104-107). The batch equation is linear, so it
- * restricts to any subset of the items: ONE range-tagged MSM pass evaluates it over about 32
+ * restricts to any subset of the items: ONE range-tagged MSM pass evaluates it over about 128
  * contiguous ranges by default (edc_set_fallback_shape; same z, same k, the decoded points of the
  * batch prefix); ranges whose
  * [8]*check is not the identity, or that hold an item with an undecodable R / key or a

@@ -345,7 +345,7 @@ def _dev_batch(torch, it, dev):
 
 
 @pytest.mark.parametrize("b", golden("batches.json")["batches"], ids=lambda b: b["name"])
-@pytest.mark.parametrize("shape", [(32, 10), (1024, 8)])
+@pytest.mark.parametrize("shape", [(32, 10), (128, 9), (1024, 8)])
 def test_batch_then_fallback_fixture(engine, b, shape):
     """edc_batch_verify_fallback_device (batch, then the one-pass grouped fallback and the quad
     per-item kernel on the failing ranges) returns the fixture's batch code, [8]*check and, for a
@@ -366,7 +366,7 @@ def test_batch_then_fallback_fixture(engine, b, shape):
         rc = lib.edc_batch_verify_fallback_device(engine.ctx, n, vk.data_ptr(), sg.data_ptr(), mg.data_ptr(),
                                                   off.data_ptr(), bytes.fromhex(b["z_seed"]), v, ctypes.byref(cnt), c8)
     finally:
-        lib.edc_set_fallback_shape(engine.ctx, 32, 10)
+        lib.edc_set_fallback_shape(engine.ctx, 128, 9)
     assert rc == b["expect_code"]
     if b["expect_check8"] is not None:
         assert c8.raw.hex() == b["expect_check8"]

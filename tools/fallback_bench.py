@@ -30,13 +30,14 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--keycache", action="store_true", help="also time with the validator keys in the key cache")
     ap.add_argument("--shapes", default="", help="sweep fallback shapes 'ranges:bits,...' (edc_set_fallback_shape)")
+    ap.add_argument("--lib", default=None, help="A/B build of libedc.so (measurement only)")
     args = ap.parse_args()
     import torch
     import bench
     dev = torch.device("cuda:0")
     torch.zeros(1, device=dev)
     pkg = bench.load_pkg()
-    eng = pkg.Engine(0)
+    eng = pkg.Engine(0, lib_path=args.lib)
     lib = eng.lib
     n = args.n
     with open(os.path.join(ROOT, "tests", "golden", "zip215_small_order.json")) as f:
@@ -96,7 +97,7 @@ def main():
         eng._check(lib.edc_set_fallback_shape(eng.ctx, r, b))
         out.setdefault("shapes", {})[sh] = run_all()
     if args.shapes:
-        eng._check(lib.edc_set_fallback_shape(eng.ctx, 32, 10))
+        eng._check(lib.edc_set_fallback_shape(eng.ctx, 128, 9))
     if args.keycache and args.keys:
         keys = bytes(vk[:32 * args.keys].cpu().tolist())
         t0 = time.perf_counter()
