@@ -423,6 +423,9 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
 #ifndef EDC_ACC_OCC
 #define EDC_ACC_OCC 4
 #endif
+#ifndef EDC_ACC_HOIST
+#define EDC_ACC_HOIST 0   // measurement knob: let the compiler hoist the DMA piece map (needs VGPRs)
+#endif
 #ifndef EDC_ACC_PROBE
 #define EDC_ACC_PROBE 0   // measurement knob: 1 = no row gathers after the first round, 2 = no LDS row reads either
 #endif
@@ -482,7 +485,9 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
   }
   // one round of row gathers: the wave's 64 rows (one per lane, `row`) -> wrows, row-major
   auto gather_rows = [&](uint32_t row) {
+#if !EDC_ACC_HOIST
     asm volatile("" : "+v"(pmap0), "+v"(pmap1));   // unpacked each round, never hoisted (VGPRs)
+#endif
 #pragma unroll
     for (int k = 0; k < ROW_PIECES; ++k) {
       const uint32_t src = k < 5 ? (pmap0 >> (6 * k)) & 63u : (pmap1 >> (6 * (k - 5))) & 63u;
