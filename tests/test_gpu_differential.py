@@ -29,11 +29,11 @@ def oc():
     return oracle_c
 
 
-def _batch(engine, rnd, n):
+def _batch(engine, rnd, n, hard=None):
     """Mixed items; "hard" batches also hold items rejected before the MSM (undecodable R / key,
     s >= l, a flipped R byte), "soft" ones only items whose rejection the MSM must find (a wrong
     message, a flipped low byte of s), so large failing batches compare a non-identity check8."""
-    hard = rnd.random() < 0.35
+    hard = rnd.random() < 0.35 if hard is None else hard
     nkeys = rnd.choice([1, 3, 17, n])
     seeds = [rnd.randbytes(32) for _ in range(nkeys)]
     msgs = [rnd.randbytes(rnd.choice([0, 1, 32, 111, 112, 120, 200, rnd.randrange(0, 400)])) for _ in range(n)]
@@ -122,3 +122,22 @@ def test_mixed_multi_union_vs_oracle(engine, oc, seed):
                                                  b"".join(msgs[lo:hi]), o, zseed, parts=2, z_base=lo)
             assert verdicts[b] == ec, (seed, trial, b)
             assert c8s[b] == (e8 if e8 is not None else bytes(32)), (seed, trial, b)
+
+
+@pytest.mark.parametrize("n", [16384, 131072])
+def test_large_mixed_batch_vs_oracle(engine, oc, n):
+    """One larger mixed batch (larger MSM plans: 12-15-bit windows, parts, sub-bins) against the
+    threaded C oracle: verdict and [8]*check, message and prehashed paths."""
+    rnd = random.Random(n)
+    vks, sigs, msgs = _batch(engine, rnd, n, hard=False)
+    zseed = rnd.randbytes(32)
+    offs = [0]
+    for m in msgs:
+        offs.append(offs[-1] + len(m))
+    ec, e8, secs = oc.batch_verify_parallel(b"".join(vks), b"".join(sigs), b"".join(msgs), offs, zseed)
+    code, c8 = engine.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True)
+    print(f"\n[differential-large] n {n}: code {code}, evaluated {e8 is not None}, oracle {secs:.2f} s")
+    assert code == ec
+    assert c8 == (e8 if e8 is not None else bytes(32))
+    ks = engine.challenge(vks, sigs, msgs)
+    assert engine.batch_verify_prehashed(vks, sigs, ks, z_seed=zseed, want_check8=True) == (code, c8)
