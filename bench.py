@@ -370,6 +370,7 @@ def main():
     lib.edc_set_timing(eng.ctx, 1)
     names = [lib.edc_timing_name(i).decode() for i in range(7)]
     acc = [0.0] * 7
+    acc_ms, acc_entries = [], []      # k_msm_accum_dma alone (edc_last_msm_accum)
     for _ in range(max(1, args.profile_steps)):
         rc = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
                                          off.data_ptr(), zseed, base, None, None)
@@ -378,6 +379,11 @@ def main():
         lib.edc_last_timings(eng.ctx, buf, 7)
         for i in range(7):
             acc[i] += buf[i] / max(1, args.profile_steps)
+        if hasattr(lib, "edc_last_msm_accum"):
+            a_ms, a_ent = ctypes.c_float(0), ctypes.c_uint64(0)
+            if lib.edc_last_msm_accum(eng.ctx, ctypes.byref(a_ms), ctypes.byref(a_ent)) == 0:
+                acc_ms.append(a_ms.value)
+                acc_entries.append(a_ent.value)
     # the same in-flight loop once more with HIP events on (still outside the timed region): the
     # dominant kernel's duration while it shares the GPU with the other in-flight batches (this is
     # what a kernel trace of the default command averages; no collectives, every rank alike)
@@ -493,6 +499,19 @@ def main():
                                 "frac": round(sha_blocks / (phases["challenge_sha512"] * 1e-3) / SHA_PEAK_BLOCKS, 4),
                                 "valu_per_block": SHA_VALU_PER_BLOCK, "bound": "valu issue (integer)"}
             if phases["challenge_sha512"] > 0 else None,
+            # k_msm_accum_dma against the same mad roofline: one signed mixed addition per digit
+            # entry, 7 M = 448 algorithmic v_mad_u64_u32; 7 x 99 = 693 executed in
+            # radix 2^29. Duration: HIP events around the kernel in the instrumented batches.
+            "roofline_msm_accum": ({"kernel": "k_msm_accum_dma", "additions_per_launch": acc_entries[-1],
+                                    "avg_launch_ms": round(sum(acc_ms) / len(acc_ms), 4),
+                                    "achieved": round(acc_entries[-1] * 448 / (sum(acc_ms) / len(acc_ms) * 1e-3) / 1e12, 3),
+                                    "peak": round(PEAK_TMAD, 2), "unit": "T v_mad_u64_u32/s",
+                                    "frac": round(acc_entries[-1] * 448 / (sum(acc_ms) / len(acc_ms) * 1e-3) / 1e12
+                                                  / PEAK_TMAD, 4),
+                                    "executed_mad_frac": round(acc_entries[-1] * 693 / (sum(acc_ms) / len(acc_ms) * 1e-3)
+                                                               / 1e12 / PEAK_TMAD, 4),
+                                    "alg_mad_per_addition": 448}
+                                   if acc_ms and acc_ms[-1] > 0 else None),
             "hbm_view": ({"achieved_gbs": round(traffic / (dom_ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
                           "frac": round(traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)} if traffic else None),
             "phases_ms": phases,

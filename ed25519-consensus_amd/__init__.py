@@ -43,6 +43,7 @@ ABI_SYMBOLS = [
     "edc_sign_device", "edc_chacha_fill_device", "edc_reserve", "edc_set_timing", "edc_last_timings", "edc_timing_name",
     "edc_synchronize", "edc_vk_validate", "edc_keycache_load", "edc_keycache_clear", "edc_keycache_size",
     "edc_keycache_add", "edc_set_multi_union", "edc_multi_union_stats", "edc_batch_submit_prehashed_indexed",
+    "edc_last_msm_accum",
     "edc_set_key_grouping", "edc_set_key_split", "edc_batch_submit", "edc_batch_submit_indexed", "edc_batch_verify_fallback_device",
     "edc_set_msm_shape", "edc_set_msm_bin_entries", "edc_set_fallback_shape", "edc_create_multi", "edc_destroy_multi", "edc_multi_size",
     "edc_multi_context", "edc_multi_last_error", "edc_multi_batch_verify", "edc_multi_batch_verify_fallback",
@@ -193,6 +194,8 @@ def load_library(path=None):
                                                   ctypes.POINTER(ctypes.c_uint64)]
             lib.edc_keycache_add.restype = ctypes.c_int64
             lib.edc_keycache_add.argtypes = [c_vp, c_sz, c_u8p, c_vp]
+            lib.edc_last_msm_accum.restype = ctypes.c_int
+            lib.edc_last_msm_accum.argtypes = [c_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint64)]
             lib.edc_batch_submit_prehashed_indexed.restype = ctypes.c_int64
             lib.edc_batch_submit_prehashed_indexed.argtypes = [c_vp, c_sz, ctypes.POINTER(ctypes.c_uint32), c_u8p,
                                                                c_u8p, c_u8p, ctypes.c_uint64, ctypes.c_int]

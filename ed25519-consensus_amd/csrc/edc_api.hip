@@ -85,6 +85,7 @@ struct Slot {
   uint8_t* mb_bad = nullptr;
   size_t mb_cap_acc = 0, mb_cap_terms = 0;
   uint32_t nmulti = 0;
+  uint32_t acc_nbin = 0;        // bins of the last enqueued single-batch MSM (timing report)
   // union-first multi launch (edc_set_multi_union): the launch ran as ONE batch over all nb * n_per
   // items; its arguments are kept (device inputs are borrowed until the wait) to rerun it batch by
   // batch when that union fails
@@ -97,6 +98,7 @@ struct Slot {
   uint64_t mu_zbase = 0;
   int mu_compress = 0;
   hipEvent_t ev[PH_N + 1] = {};
+  hipEvent_t ev_acc[2] = {};    // timed batches: around k_msm_accum_dma (edc_last_msm_accum)
   // EDC_DUAL_STREAM builds: the decode runs on a second stream beside SHA-512 / coefficients /
   // binning (joined before the accumulation)
   hipStream_t st2 = nullptr;
@@ -134,6 +136,8 @@ struct edc_ctx {
   size_t comb_cap = 0;
   bool timing = false;
   float last_ms[PH_N] = {};
+  float last_acc_ms = 0.f;      // k_msm_accum_dma of the last timed batch
+  uint32_t last_acc_entries = 0;
   int nlast = 0;
   int64_t next_ticket = 0;
   int nslots = kSlots;          // in-flight slots the submissions rotate over (edc_set_slots)
@@ -245,6 +249,7 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   CK(dalloc(&s.d_out, 256 * kMultiMax));
   CK(hipHostMalloc((void**)&s.h_out, 256 * kMultiMax));
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
+  for (int p = 0; p < 2; ++p) CK(hipEventCreate(&s.ev_acc[p]));
 #if EDC_DUAL_STREAM
   // 1: every slot; 2: slot 0 only (the synchronous calls' slot), so the pipelined slots keep one
   // hardware queue each (past ~16 user queues per GPU the scheduler time-slices them).
@@ -728,7 +733,9 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
-                    s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0);
+                    s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0, s.timed ? s.ev_acc[0] : nullptr,
+                    s.timed ? s.ev_acc[1] : nullptr);
+  s.acc_nbin = P.nbin();
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
   // the final kernel stores the result block to d_out and straight into the pinned h_out
   if (EDC_RUN(128)) launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out, s.h_out);
@@ -941,6 +948,13 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
   if (s.timed) {
     for (int p = 0; p < PH_N; ++p) CK(hipEventElapsedTime(&ctx->last_ms[p], s.ev[p], s.ev[p + 1]));
     ctx->nlast = PH_N;
+    CK(hipEventElapsedTime(&ctx->last_acc_ms, s.ev_acc[0], s.ev_acc[1]));
+    uint32_t o = 0, c = 0;             // digit entries the accumulation added: the last bin's end
+    if (s.acc_nbin) {
+      CK(hipMemcpy(&o, s.offsets + s.acc_nbin - 1, sizeof(o), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(&c, s.counts + s.acc_nbin - 1, sizeof(c), hipMemcpyDeviceToHost));
+    }
+    ctx->last_acc_entries = o + c;
   }
   const int verdict = reinterpret_cast<int*>(s.h_out)[0];
   const int bad = reinterpret_cast<int*>(s.h_out)[1];
@@ -1054,6 +1068,8 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
+    for (hipEvent_t e : s.ev_acc)
+      if (e) (void)hipEventDestroy(e);
     if (s.st) (void)hipStreamDestroy(s.st);
     if (s.st2) (void)hipStreamDestroy(s.st2);
     if (s.ev_keys) (void)hipEventDestroy(s.ev_keys);
@@ -1067,6 +1083,8 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.h_out) (void)hipHostFree(s.h_out);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
+    for (hipEvent_t e : s.ev_acc)
+      if (e) (void)hipEventDestroy(e);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
@@ -1950,6 +1968,13 @@ int edc_last_timings(const edc_ctx* ctx, float* ms, int cap) {
 }
 
 const char* edc_timing_name(int i) { return (i >= 0 && i < PH_N) ? kPhaseNames[i] : ""; }
+
+int edc_last_msm_accum(const edc_ctx* ctx, float* ms, uint64_t* entries) {
+  if (!ctx || !ctx->nlast) return EDC_ERR_ARG;
+  if (ms) *ms = ctx->last_acc_ms;
+  if (entries) *entries = ctx->last_acc_entries;
+  return 0;
+}
 
 int edc_synchronize(edc_ctx* ctx) {
   if (!ctx) return EDC_ERR_ARG;

@@ -1010,15 +1010,18 @@ static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t); 
 
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
-                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip) {
+                       uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip,
+                       hipEvent_t acc_begin, hipEvent_t acc_end) {
   // one workgroup per bin (sort, then accumulation), then the lane-parallel bin reductions
   // (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
   if (!(probe_skip & 256))
     hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end,
                        buckets);
+  if (acc_begin) (void)hipEventRecord(acc_begin, st);      // timed batches: the accumulation alone
   if (!(probe_skip & 32))
     hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
                        buckets, heads, slice_W, slice_T);
+  if (acc_end) (void)hipEventRecord(acc_end, st);
   if (probe_skip & 64) return;
   if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);

@@ -407,6 +407,10 @@ int edc_reserve(edc_ctx* ctx, size_t n);
 void edc_set_timing(edc_ctx* ctx, int enable);
 int edc_last_timings(const edc_ctx* ctx, float* ms, int cap);
 const char* edc_timing_name(int i);
+/* The last timed batch's accumulation kernel alone (k_msm_accum_dma, between HIP events on its
+ * stream): duration in ms and the number of digit entries it added (one signed mixed addition
+ * each), for the accumulation's own roofline in bench.py. EDC_ERR_ARG before any timed batch. */
+int edc_last_msm_accum(const edc_ctx* ctx, float* ms, uint64_t* entries);
 
 /* Synchronize the context stream (for callers that time around device calls). */
 int edc_synchronize(edc_ctx* ctx);
