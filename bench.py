@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--prehashed", action="store_true",
                     help="time edc_batch_submit_prehashed_device: items carry their queue-time k (the reference's "
                          "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
+    ap.add_argument("--scatter-stage", type=int, default=0,
+                    help="measurement only: cap the binning scatter's LDS stage (entries; edc_debug_set_scatter_stage)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -265,6 +267,8 @@ def main():
     # queues) exist beside RCCL's own in a multi-rank run; a build with fewer slots keeps its count
     if nmb > 1:
         eng.set_multi_union(not args.multi_exact)
+    if args.scatter_stage:
+        eng._check(eng.lib.edc_debug_set_scatter_stage(args.scatter_stage))
     if eng.lib.edc_set_slots(eng.ctx, args.inflight) < 0 and sharing > 1:
         raise RuntimeError("cannot split the GPU's slots between the ranks sharing it")
     t_gen = time.perf_counter()
