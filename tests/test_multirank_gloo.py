@@ -54,9 +54,10 @@ def _worker(rank, world, port, name, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["mixed_corpus_one_bad", "repeated_keys_varlen", "undecodable_R"])
-def test_two_rank_sharded_verify(tmp_path, name):
-    world = 2
+@pytest.mark.parametrize("name,world", [("mixed_corpus_one_bad", 2), ("repeated_keys_varlen", 2), ("undecodable_R", 2),
+                                        ("mixed_corpus_one_bad", 4), ("repeated_keys_varlen", 8)])
+def test_two_rank_sharded_verify(tmp_path, name, world):
+    """world_size 2 (and 4 / 8 ranks, the driver's scaling shapes) over gloo."""
     out = str(tmp_path / "res")
     mp.start_processes(_worker, args=(world, _free_port(), name, out), nprocs=world, join=True,
                        start_method="spawn")
