@@ -1012,7 +1012,7 @@ edc_ctx* edc_create(int device) {
   }
   (void)hipGetLastError();   // launch checks below must not see an earlier, unrelated failure
   bool ok = hipSetDevice(device) == hipSuccess && msm_init_device() == hipSuccess && init_slot(ctx, ctx->slot[0]) == 0 &&
-            dalloc(&ctx->btab, BTAB_ENTRIES * NIELS_WORDS) == hipSuccess;
+            dalloc(&ctx->btab, BTAB_TOTAL * NIELS_WORDS) == hipSuccess;
   if (ok) {
     launch_init_btable(ctx->st(), ctx->btab);
     ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(ctx->st()) == hipSuccess;

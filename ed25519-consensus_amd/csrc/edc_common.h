@@ -153,6 +153,11 @@ __host__ __device__ __forceinline__ uint32_t split_hi_point(uint32_t n, uint32_t
 __host__ __device__ __forceinline__ uint32_t split_b_hi_point(uint32_t n, uint32_t m) { return 1 + n + m; }
 
 constexpr int BTAB_ENTRIES = 8;
+// radix-256 comb of B behind the 8 multiples in the same table: entry 8 + 128 j + d - 1 =
+// [d 256^j]B (j = 0..31, d = 1..128), affine Niels; the per-item kernels take [s]B from it with 32
+// additions and no doublings (instead of 64 additions inside the doubling loop)
+constexpr int B256_POS = 32, B256_MULT = 128, B256_ENTRIES = B256_POS * B256_MULT;
+constexpr int BTAB_TOTAL = BTAB_ENTRIES + B256_ENTRIES;
 constexpr uint32_t COEF_CHUNK = 2048;   // signatures per k_coef workgroup (range sizes are multiples)   // context table [1..8]B (per-item fallback, signer)
 
 // Per-item failure bits written by the prefix kernels (the grouped fallback reads them).

@@ -64,6 +64,35 @@ __device__ __forceinline__ int radix16_digit(const uint32_t s[8], uint64_t carri
   return nib + cin - 16 * (int)((carries >> j) & 1);
 }
 
+// signed radix-256 digits of a scalar < 2^253 (s < l): 32 digits in [-127, 128]; bit j of the
+// mask is the carry out of byte j (the digit was lowered by 256)
+__device__ __forceinline__ uint32_t radix256_carries(const uint32_t s[8]) {
+  uint32_t m = 0, carry = 0;
+  for (int j = 0; j < 31; ++j) {
+    const uint32_t v = ((s[j >> 2] >> (8 * (j & 3))) & 255u) + carry;
+    carry = v > 128;
+    m |= carry << j;
+  }
+  return m;
+}
+__device__ __forceinline__ int radix256_digit(const uint32_t s[8], uint32_t carries, int j) {
+  const int byte = (int)((word_at(s, j >> 2) >> (8 * (j & 3))) & 255u);
+  const int cin = j ? (int)((carries >> (j - 1)) & 1u) : 0;
+  return byte + cin - 256 * (int)((carries >> j) & 1u);
+}
+// acc + [s]B from the radix-256 comb (btab entries BTAB_ENTRIES..): 32 signed additions
+__device__ __forceinline__ ge_p3 add_base_comb(ge_p3 acc, const uint32_t s[8], const uint32_t* __restrict__ btab) {
+  const uint32_t sc = radix256_carries(s);
+  const uint32_t* comb = btab + (size_t)BTAB_ENTRIES * NIELS_WORDS;
+  for (int j = 0; j < B256_POS; ++j) {
+    const int b = radix256_digit(s, sc, j);
+    const int bi = b < 0 ? -b : b;
+    const ge_niels nb = bi ? ld_niels(comb, j * B256_MULT + bi - 1) : ge_niels_identity();
+    acc = ge_madd_sgn(acc, nb, b < 0);
+  }
+  return acc;
+}
+
 __device__ __forceinline__ ge_cached cached_identity() {
   ge_cached c; c.ypx = fe_one(); c.ymx = fe_one(); c.Z = fe_one(); c.T2d = fe_zero(); return c;
 }
@@ -90,7 +119,7 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
     acc = ge_add_cached(acc, c);
     st_cached(tab + i * EXT_WORDS, ge_to_cached(acc));
   }
-  const uint64_t kc = radix16_carries(k), sc = radix16_carries(s);
+  const uint64_t kc = radix16_carries(k);
   acc = ge_identity();
   for (int j = 63; j >= 0; --j) {
     if (j != 63) {
@@ -104,35 +133,26 @@ __device__ ge_p3 double_scalar_mul(const uint32_t k[8], const ge_p3& P, const ui
     ge_cached q = ai ? ld_cached(tab + (ai - 1) * EXT_WORDS) : cached_identity();
     if (a < 0) q = ge_cached_neg(q);
     acc = ge_add_cached(acc, q);
-    EDC_SCHED_FENCE();
-    int b = radix16_digit(s, sc, j);
-    int bi = b < 0 ? -b : b;
-    ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
-    acc = ge_madd_sgn(acc, nb, b < 0);
   }
-  return acc;
+  return add_base_comb(acc, s, btab);                // [s]B: 32 comb additions, no doublings
 }
 
 // verdict codes: 0 Ok, 1 InvalidSignature, 2 MalformedPublicKey
-// Cached key (keycache.h): [s]B - [k]A from the key's and B's comb tables, 64 positions of
-// signed radix-16 digits, one affine Niels record per digit and NO doublings (the joint
-// windowed loop below needs 252). Zero digits add the identity (branch-free across the wave).
+// Cached key (keycache.h): [s]B - [k]A from comb tables and NO doublings (the joint windowed
+// loop below needs 252): -[k]A over the key's 64 radix-16 positions, [s]B over B's 32 radix-256
+// positions (btab). One affine Niels record per digit; zero digits add the identity
+// (branch-free across the wave).
 __device__ ge_p3 comb_double_base(const uint32_t k[8], const uint32_t s[8], const uint32_t* __restrict__ acomb,
-                                  const uint32_t* __restrict__ bcomb) {
-  const uint64_t kc = radix16_carries(k), sc = radix16_carries(s);
+                                  const uint32_t* __restrict__ btab) {
+  const uint64_t kc = radix16_carries(k);
   ge_p3 acc = ge_identity();
   for (int j = 0; j < COMB_POS; ++j) {
     const int a = radix16_digit(k, kc, j);
     const int ai = a < 0 ? -a : a;
     ge_niels q = ai ? ld_niels(acomb, j * COMB_MULT + ai - 1) : ge_niels_identity();
     acc = ge_madd_sgn(acc, q, a > 0);          // -[k]A
-    EDC_SCHED_FENCE();
-    const int b = radix16_digit(s, sc, j);
-    const int bi = b < 0 ? -b : b;
-    ge_niels nb = bi ? ld_niels(bcomb, j * COMB_MULT + bi - 1) : ge_niels_identity();
-    acc = ge_madd_sgn(acc, nb, b < 0);
   }
-  return acc;
+  return add_base_comb(acc, s, btab);
 }
 
 // Per-item verification of the items whose key is registered in the context's cache (the
@@ -142,7 +162,7 @@ __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_comb(uint32_t n, const
                                                                const uint8_t* __restrict__ sig,
                                                                const uint32_t* __restrict__ kscal,
                                                                uint8_t* __restrict__ verdict, KeyCacheView kcache,
-                                                               const uint32_t* __restrict__ bcomb) {
+                                                               const uint32_t* __restrict__ btab) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8];
@@ -160,7 +180,7 @@ __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_comb(uint32_t n, const
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
-  const ge_p3 Rp = comb_double_base(k, sw, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS, bcomb);
+  const ge_p3 Rp = comb_double_base(k, sw, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS, btab);
   verdict[i] = ge_is_identity(ge_mul_by_cofactor(ge_add(R, ge_neg(Rp)))) ? 0 : 1;
 }
 
@@ -242,9 +262,9 @@ __global__ void __launch_bounds__(64) k_verify_quad(uint32_t n, const uint8_t* _
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
-  const uint64_t kc = radix16_carries(k), sc = radix16_carries(sw);
+  const uint64_t kc = radix16_carries(k);
   acc = ge_identity();
-  for (int j = 63; j >= 0; --j) {                  // R' = [k](-A) + [s]B
+  for (int j = 63; j >= 0; --j) {                  // R' = [k](-A) + [s]B: [k](-A) here
     if (j != 63) {
       acc = quad_dbl(acc);
       acc = quad_dbl(acc);
@@ -256,11 +276,17 @@ __global__ void __launch_bounds__(64) k_verify_quad(uint32_t n, const uint8_t* _
     ge_cached qa = ai ? ld_cached(tab + (ai - 1) * EXT_WORDS) : cached_identity();
     if (a < 0) qa = ge_cached_neg(qa);
     acc = quad_add_cached(acc, qa);
-    const int b = radix16_digit(sw, sc, j);
-    const int bi = b < 0 ? -b : b;
-    ge_niels nb = bi ? ld_niels(btab, bi - 1) : ge_niels_identity();
-    if (b < 0) nb = ge_niels_neg(nb);
-    acc = quad_madd(acc, nb);
+  }
+  {                                                // + [s]B: 32 radix-256 comb additions
+    const uint32_t sc = radix256_carries(sw);
+    const uint32_t* comb = btab + (size_t)BTAB_ENTRIES * NIELS_WORDS;
+    for (int j = 0; j < B256_POS; ++j) {
+      const int b = radix256_digit(sw, sc, j);
+      const int bi = b < 0 ? -b : b;
+      ge_niels nb = bi ? ld_niels(comb, j * B256_MULT + bi - 1) : ge_niels_identity();
+      if (b < 0) nb = ge_niels_neg(nb);
+      acc = quad_madd(acc, nb);
+    }
   }
   ge_p3 d = quad_add(ld_ext(tab + 8 * EXT_WORDS), ge_neg(acc));
   d = quad_dbl(quad_dbl(quad_dbl(d)));
@@ -285,6 +311,17 @@ __device__ ge_p3 base_mul(const uint32_t x[8], const uint32_t* btab) {
     acc = ge_madd_sgn(acc, nb, b < 0);
   }
   return acc;
+}
+
+// the radix-256 comb of B (btab entries BTAB_ENTRIES..): lane j*128 + d-1 -> [d 256^j]B,
+// computed from the 8 multiples already in btab; a context builds it once
+__global__ void __launch_bounds__(256) k_init_b256(uint32_t* btab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint32_t)B256_ENTRIES) return;
+  const uint32_t j = i / B256_MULT, d = i % B256_MULT + 1;
+  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  x[j >> 2] = d << (8 * (j & 3));                  // d <= 128 fits byte j
+  st_niels(btab + (size_t)BTAB_ENTRIES * NIELS_WORDS, i, to_niels(base_mul(x, btab)));
 }
 
 __device__ __forceinline__ void words_to_bytes32(const uint32_t w[8], uint8_t* out) {
@@ -417,6 +454,7 @@ static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b -
 
 void launch_init_btable(hipStream_t st, uint32_t* btab) {
   hipLaunchKernelGGL(k_init_btable, dim3(1), dim3(64), 0, st, btab);
+  hipLaunchKernelGGL(k_init_b256, dim3(cdiv(B256_ENTRIES, 256)), dim3(256), 0, st, btab);
 }
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,
                           const uint32_t* k, const uint32_t* btab, uint32_t* vtab, uint8_t* verdict,
@@ -424,7 +462,7 @@ void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const u
   if (!n) return;
   if (kc.table)
     hipLaunchKernelGGL(k_verify_comb, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, verdict, kc,
-                       bcomb);
+                       btab);
   hipLaunchKernelGGL(k_verify_single, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, btab,
                      vtab, verdict, kc);
 }
@@ -433,7 +471,7 @@ void launch_verify_quad(hipStream_t st, uint32_t n, const uint8_t* vk, const uin
   if (!n) return;
   if (kc.table)
     hipLaunchKernelGGL(k_verify_comb, dim3(cdiv(n, SV_THREADS)), dim3(SV_THREADS), 0, st, n, vk, sig, k, verdict, kc,
-                       bcomb);
+                       btab);
   hipLaunchKernelGGL(k_verify_quad, dim3(cdiv(4ull * n, 64)), dim3(64), 0, st, n, vk, sig, k, btab, verdict, kc);
 }
 void launch_kc_decode(hipStream_t st, uint32_t m, const uint32_t* keys, uint32_t* ext, uint8_t* ok) {
