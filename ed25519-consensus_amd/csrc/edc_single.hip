@@ -64,7 +64,8 @@ __device__ __forceinline__ int radix16_digit(const uint32_t s[8], uint64_t carri
   return nib + cin - 16 * (int)((carries >> j) & 1);
 }
 
-// signed radix-256 digits of a scalar < 2^253 (s < l): 32 digits in [-127, 128]; bit j of the
+// signed radix-256 digits of a scalar whose top byte is <= 127 (s < l; a clamped secret scalar,
+// bit 255 clear): 32 digits in [-127, 128], no carry out of byte 31; bit j of the
 // mask is the carry out of byte j (the digit was lowered by 256)
 __device__ __forceinline__ uint32_t radix256_carries(const uint32_t s[8]) {
   uint32_t m = 0, carry = 0;
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(64) k_sign(uint32_t n, const uint8_t* __restri
     a[j] = (uint32_t)ab[4 * j] | ((uint32_t)ab[4 * j + 1] << 8) | ((uint32_t)ab[4 * j + 2] << 16) |
            ((uint32_t)ab[4 * j + 3] << 24);
   uint32_t Aw[8];
-  ge_compress(base_mul(a, btab), Aw);
+  ge_compress(add_base_comb(ge_identity(), a, btab), Aw);   // [a]B: clamped a < 2^255, top digit <= 128
   uint8_t Ab[32];
   words_to_bytes32(Aw, Ab);
   const uint64_t o0 = off[i], o1 = off[i + 1];
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(64) k_sign(uint32_t n, const uint8_t* __restri
   sha512_src(rs, rd);
   sc r = sc_from_digest(rd);
   uint32_t Rw[8];
-  ge_compress(base_mul(r.v, btab), Rw);
+  ge_compress(add_base_comb(ge_identity(), r.v, btab), Rw);  // [r]B from the radix-256 comb
   uint8_t Rb[32];
   words_to_bytes32(Rw, Rb);
   uint8_t kd[64];
