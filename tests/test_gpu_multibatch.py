@@ -248,3 +248,25 @@ def test_multi_argument_errors(engine, edc):
     with pytest.raises(edc.EngineError):
         engine.batch_wait_multi(t, 3)             # wrong batch count
     assert engine.batch_wait_multi(t, 2)[1] == [0, 0]
+
+
+def test_multi_union_with_key_cache(engine):
+    """Union-first launches on a context whose key cache holds the validators (the union then runs
+    with split coefficients): the same per-batch results as single batches, valid and failing."""
+    torch = pytest.importorskip("torch")
+    nb, n_per = 4, 2048
+    vks, sigs, msgs, offs, d = _make(engine, torch, nb, n_per, 30, seed=313, spoil=[(3 * n_per + 17, "msg")])
+    zseed = bytes([0x7E]) * 32
+    engine.set_multi_union(True)
+    try:
+        engine.keycache_load(list(dict.fromkeys(vks)))
+        for _ in range(2):                            # the second launch plans split coefficients
+            res = _multi(engine, d, nb, n_per, zseed, 0)
+            assert res[1] == [0, 0, 0, 1]
+            _check_against_single(engine, torch, d, nb, n_per, offs, zseed, 0, res)
+        valid = _make(engine, torch, nb, n_per, 30, seed=313)[4]
+        for _ in range(2):
+            res = _multi(engine, valid, nb, n_per, zseed, 0)
+            assert res[0] == 0 and res[2] == [IDENTITY] * nb
+    finally:
+        engine.keycache_clear()
