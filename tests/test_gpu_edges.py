@@ -159,3 +159,33 @@ def test_device_chacha_two_block_known_answer(engine):
     blk = (1 << 32) + 5
     assert engine.lib.edc_chacha_fill_device(engine.ctx, key, blk, 2, out.data_ptr()) == 0
     assert bytes(out.cpu().tolist()) == oracle.chacha20_keystream(key, 128, blk)
+
+
+def test_timing_report_and_accum_counts(edc):
+    """edc_set_timing / edc_last_timings / edc_last_msm_accum (the bench's phase times and the
+    accumulation's own roofline): an error before any timed batch, then the phase names, positive
+    durations, and a digit-entry count within what the plan can add (at most one entry per term
+    and window: 2n + 1 terms over at most 29 windows for a small distinct-key batch)."""
+    import ctypes
+    eng = edc.Engine(0)
+    try:
+        lib = eng.lib
+        ms, ent = ctypes.c_float(0), ctypes.c_uint64(0)
+        assert lib.edc_last_msm_accum(eng.ctx, ctypes.byref(ms), ctypes.byref(ent)) < 0
+        rnd = __import__("random").Random(5)
+        n = 64
+        seeds = [rnd.randbytes(32) for _ in range(n)]
+        msgs = [rnd.randbytes(40) for _ in range(n)]
+        vks, sigs = eng.sign(seeds, msgs)
+        lib.edc_set_timing(eng.ctx, 1)
+        code, _ = eng.batch_verify(vks, sigs, msgs, z_seed=bytes(32))
+        assert code == 0
+        names = [lib.edc_timing_name(i).decode() for i in range(7)]
+        assert "decompress_R" in names and "challenge_sha512" in names
+        buf = (ctypes.c_float * 7)()
+        assert lib.edc_last_timings(eng.ctx, buf, 7) == 7 and all(x >= 0 for x in buf)
+        assert lib.edc_last_msm_accum(eng.ctx, ctypes.byref(ms), ctypes.byref(ent)) == 0
+        assert ms.value > 0
+        assert ent.value > 0 and ent.value <= (n + n + 1) * 29
+    finally:
+        eng.close()
