@@ -625,6 +625,18 @@ def _as_bytes(x, n):
     return b
 
 
+_L = (1 << 252) + 27742317777372353535851937790883648493    # the group order l
+
+
+def _canonical_k(k):
+    """A prehashed challenge as the reference's Item holds it: Scalar::from_hash output, < l
+    (src/batch.rs:82-94). Anything else is an argument error, never a verdict."""
+    b = _as_bytes(k, 32)
+    if int.from_bytes(b, "little") >= _L:
+        raise ValueError("prehashed k is not a canonical scalar (must be < l)")
+    return b
+
+
 class Signature:
     """reference src/signature.rs:8-62: 64 bytes R || s, not validated at parse time."""
 
@@ -686,7 +698,12 @@ class VerificationKey:
     """reference src/verification_key.rs:106-258. try_from decodes A on the GPU once and keeps it:
     the reference stores minus_A in the object (:111-114, :160-175); here the decoded point and its
     fixed-base table go into the engine's key cache (edc_keycache_add), where every later verify,
-    batch or fallback of that engine finds them (`cached`). keep_decoded=False only validates."""
+    batch or fallback of that engine finds them (`cached`). keep_decoded=False only validates;
+    True always adds; None (the default) adds while the engine's cache holds fewer than
+    AUTO_CACHE_KEYS keys, so keys parsed from untrusted input cannot grow device memory without
+    bound. Keys that do not decode are never added (edc_keycache_add)."""
+
+    AUTO_CACHE_KEYS = 1024          # 64 MB of comb tables
 
     __slots__ = ("A_bytes", "_engine", "cached")
 
@@ -696,19 +713,22 @@ class VerificationKey:
         self.cached = cached
 
     @classmethod
-    def try_from(cls, data, engine=None, keep_decoded=True):
+    def try_from(cls, data, engine=None, keep_decoded=None):
         r = cls.try_from_many([data], engine, keep_decoded)[0]
         if isinstance(r, MalformedPublicKey):
             raise r
         return r
 
     @classmethod
-    def try_from_many(cls, keys, engine=None, keep_decoded=False):
+    def try_from_many(cls, keys, engine=None, keep_decoded=None):
         """Batched key ingestion: [VerificationKey or MalformedPublicKey()] per input, one launch
-        (keep_decoded: also add the keys to the engine's key cache)."""
+        (keep_decoded: also add the keys to the engine's key cache; None: while it stays under
+        AUTO_CACHE_KEYS)."""
         vkbs = [k if isinstance(k, VerificationKeyBytes) else VerificationKeyBytes(k) for k in keys]
         eng = engine or default_engine()
         encs = [v.to_bytes() for v in vkbs]
+        if keep_decoded is None:
+            keep_decoded = eng.keycache_size() + len(set(encs)) <= cls.AUTO_CACHE_KEYS
         cached = False
         if keep_decoded and encs:
             try:
@@ -773,7 +793,7 @@ class batch:  # namespace mirroring `ed25519_consensus::batch`
             if msg is None and k is None:
                 raise ValueError("an Item needs its message or its challenge k")
             self._msg = bytes(msg) if msg is not None else None
-            self.k = _as_bytes(k, 32) if k is not None else None
+            self.k = _canonical_k(k) if k is not None else None
 
         @classmethod
         def from_tuple(cls, tup):

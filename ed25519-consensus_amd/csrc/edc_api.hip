@@ -78,6 +78,7 @@ struct Slot {
   int* flags = nullptr;
   uint8_t* d_out = nullptr;     // 256-byte result block (kMultiMax of them for a multi-batch launch)
   uint8_t* h_out = nullptr;     // pinned mirror
+  uint32_t* h_acc = nullptr;    // pinned: the last bin's offset and count (timed batches' entry count)
   // several batches in one launch (edc_batch_submit_multi_device): per-(batch, key) sums, listed
   // key / B terms, per-batch bad flags; nmulti = batches of the pending launch (0: one batch)
   unsigned long long* mb_acc = nullptr;
@@ -248,6 +249,7 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   CK(dalloc(&s.flags, FLAG_COUNT));
   CK(dalloc(&s.d_out, 256 * kMultiMax));
   CK(hipHostMalloc((void**)&s.h_out, 256 * kMultiMax));
+  CK(hipHostMalloc((void**)&s.h_acc, 2 * sizeof(uint32_t)));
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
   for (int p = 0; p < 2; ++p) CK(hipEventCreate(&s.ev_acc[p]));
 #if EDC_DUAL_STREAM
@@ -736,7 +738,11 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
                     s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0, s.timed ? s.ev_acc[0] : nullptr,
                     s.timed ? s.ev_acc[1] : nullptr);
   s.acc_nbin = P.nbin();
-  if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
+  if (s.timed) {   // the accumulation's entry count, read at the wait without another sync
+    CK(hipMemcpyAsync(s.h_acc, s.offsets + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(s.h_acc + 1, s.counts + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
+  }
   // the final kernel stores the result block to d_out and straight into the pinned h_out
   if (EDC_RUN(128)) launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out, s.h_out);
   if (s.timed) (void)hipEventRecord(s.ev[PH_N], st);
@@ -949,12 +955,8 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
     for (int p = 0; p < PH_N; ++p) CK(hipEventElapsedTime(&ctx->last_ms[p], s.ev[p], s.ev[p + 1]));
     ctx->nlast = PH_N;
     CK(hipEventElapsedTime(&ctx->last_acc_ms, s.ev_acc[0], s.ev_acc[1]));
-    uint32_t o = 0, c = 0;             // digit entries the accumulation added: the last bin's end
-    if (s.acc_nbin) {
-      CK(hipMemcpy(&o, s.offsets + s.acc_nbin - 1, sizeof(o), hipMemcpyDeviceToHost));
-      CK(hipMemcpy(&c, s.counts + s.acc_nbin - 1, sizeof(c), hipMemcpyDeviceToHost));
-    }
-    ctx->last_acc_entries = o + c;
+    // digit entries the accumulation added: the last bin's end (queued on s.st at the enqueue)
+    ctx->last_acc_entries = s.acc_nbin ? s.h_acc[0] + s.h_acc[1] : 0;
   }
   const int verdict = reinterpret_cast<int*>(s.h_out)[0];
   const int bad = reinterpret_cast<int*>(s.h_out)[1];
@@ -1066,6 +1068,7 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.flags) (void)hipFree(s.flags);
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.h_acc) (void)hipHostFree(s.h_acc);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
     for (hipEvent_t e : s.ev_acc)
@@ -1081,6 +1084,7 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.flags) (void)hipFree(s.flags);
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.h_acc) (void)hipHostFree(s.h_acc);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
     for (hipEvent_t e : s.ev_acc)
@@ -1297,6 +1301,11 @@ int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
 int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* k,
                               uint8_t* verdicts) {
   if (!ctx || (n && (!vk || !sig || !k || !verdicts))) return EDC_ERR_ARG;
+  for (size_t i = 0; i < n; ++i) {        // Scalar::from_hash never yields k >= l (batch paths: FLAG_KARG)
+    uint32_t w[8];
+    memcpy(w, k + 32 * i, 32);
+    if (!sc_is_canonical(w)) { ctx->err = "prehashed k is not a canonical scalar"; return EDC_ERR_ARG; }
+  }
   CK(hipSetDevice(ctx->device));
   int rc = ensure_n(ctx, n);
   if (rc) return rc;
@@ -1751,13 +1760,20 @@ static int kc_append(edc_ctx* ctx, const std::vector<uint32_t>& neww) {
     while (table[h] != KC_EMPTY) h = (h + 1) & (T - 1);
     table[h] = c;
   }
-  if (T - 1 != ctx->kc_tmask || !ctx->kc_table) {
-    if (ctx->kc_table) (void)hipFree(ctx->kc_table);
-    ctx->kc_table = nullptr;
-    CK(dalloc(&ctx->kc_table, T));
+  // new table and scratch first: a failed allocation leaves the previous cache fully usable
+  uint32_t *ntable = nullptr, *ext = nullptr;
+  const bool new_table = T - 1 != ctx->kc_tmask || !ctx->kc_table;
+  if ((new_table && dalloc(&ntable, T) != hipSuccess) || dalloc(&ext, (size_t)(un + 1) * EXT_WORDS) != hipSuccess) {
+    (void)hipGetLastError();
+    if (ntable) (void)hipFree(ntable);
+    ctx->err = "key cache: out of device memory";
+    return EDC_ERR_NOMEM;
   }
-  uint32_t* ext = nullptr;
-  CK(dalloc(&ext, (size_t)(un + 1) * EXT_WORDS));
+  if (new_table) {
+    CK(hipStreamSynchronize(st));
+    if (ctx->kc_table) (void)hipFree(ctx->kc_table);
+    ctx->kc_table = ntable;
+  }
   CK(hipMemcpyAsync(ctx->kc_table, table.data(), T * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(ctx->kc_keys + (size_t)u0 * 8, neww.data(), neww.size() * sizeof(uint32_t),
                     hipMemcpyHostToDevice, st));
@@ -1830,9 +1846,40 @@ int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok)
   if (rc) return rc;
   std::vector<uint32_t> of, words;
   if ((rc = kc_collect(ctx, m, vk, of, words))) return rc;
-  if ((rc = kc_append(ctx, words))) return rc;
+  // keys that fail to decode (VerificationKey::try_from's MalformedPublicKey) are not added: the
+  // entry is meant for keys parsed from untrusted input, and a malformed one must not pin 64 KB of
+  // comb table. of[] is remapped to the kept keys; a dropped key reports ok = 0.
+  const uint32_t u0 = ctx->kc_m, un = (uint32_t)(words.size() / 8);
+  std::vector<uint8_t> code(un, 0);
+  if (un) {
+    hipStream_t st = ctx->st();
+    uint8_t *denc = nullptr, *dcode = nullptr;
+    if (dalloc(&denc, (size_t)un * 32) != hipSuccess || dalloc(&dcode, un) != hipSuccess) {
+      (void)hipGetLastError();
+      if (denc) (void)hipFree(denc);
+      ctx->err = "key cache: out of device memory";
+      return EDC_ERR_NOMEM;
+    }
+    CK(hipMemcpyAsync(denc, words.data(), (size_t)un * 32, hipMemcpyHostToDevice, st));
+    launch_vk_validate(st, un, denc, dcode);
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(code.data(), dcode, un, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    (void)hipFree(denc);
+    (void)hipFree(dcode);
+  }
+  std::vector<uint32_t> keep, remap(un, UINT32_MAX);
+  for (uint32_t j = 0; j < un; ++j)
+    if (code[j] == EDC_OK) {
+      remap[j] = u0 + (uint32_t)(keep.size() / 8);
+      keep.insert(keep.end(), &words[8 * j], &words[8 * j] + 8);
+    }
+  if ((rc = kc_append(ctx, keep))) return rc;
   if (ok)
-    for (size_t i = 0; i < m; ++i) ok[i] = ctx->kc_okh[of[i]];
+    for (size_t i = 0; i < m; ++i) {
+      const uint32_t c = of[i] < u0 ? of[i] : remap[of[i] - u0];
+      ok[i] = c == UINT32_MAX ? 0 : ctx->kc_okh[c];
+    }
   return ctx->kc_m;
 }
 

@@ -807,10 +807,13 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
   if (wave == 0) horner_row(c, P, 0, slice_W, win, cached, res, from, from_w);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
+    // a batch rejected by its bad flag (undecodable R / key, s >= l) reports the identity as its
+    // partial and check point: the MSM sum then holds an off-curve point, whose value depends on
+    // the order the additions ran in, and a public output must be the same on every run
+    const int bad = flags[FLAG_BAD];
+    const ge_p3 acc = bad ? ge_identity() : ld_ext(res), c8 = bad ? ge_identity() : ld_ext(res + EXT_WORDS);
     uint8_t* b = reinterpret_cast<uint8_t*>(blk);
     ext_to_canonical_bytes(acc, b + 48);
-    const int bad = flags[FLAG_BAD];
     blk[0] = (!bad && ge_is_identity(c8)) ? 0u : 1u;
     blk[1] = (uint32_t)bad;
     blk[2] = (uint32_t)flags[FLAG_NKEYS];   // distinct keys seen (adaptive grouping)
@@ -902,9 +905,9 @@ __global__ void __launch_bounds__(64) k_msm_multi_final(MsmPlan P, const uint32_
   horner_row(c, P, g, slice_W, win, cached, res);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const ge_p3 acc = ld_ext(res), c8 = ld_ext(res + EXT_WORDS);
+    const int bad = rbad[g] ? 1 : 0;     // rejected by its bad flag: identity (see k_msm_final)
+    const ge_p3 acc = bad ? ge_identity() : ld_ext(res), c8 = bad ? ge_identity() : ld_ext(res + EXT_WORDS);
     ext_to_canonical_bytes(acc, reinterpret_cast<uint8_t*>(blk) + 48);
-    const int bad = rbad[g] ? 1 : 0;
     blk[0] = (!bad && ge_is_identity(c8)) ? 0u : 1u;
     blk[1] = (uint32_t)bad;
     blk[2] = (uint32_t)flags[FLAG_NKEYS];

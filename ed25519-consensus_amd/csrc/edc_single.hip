@@ -181,6 +181,7 @@ __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_comb(uint32_t n, const
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  if (!sc_is_canonical(k)) { verdict[i] = 1; return; }           // k >= l: its digits exceed the comb
   const ge_p3 Rp = comb_double_base(k, sw, kcache.comb + (size_t)ci * COMB_ENTRIES * NIELS_WORDS, btab);
   verdict[i] = ge_is_identity(ge_mul_by_cofactor(ge_add(R, ge_neg(Rp)))) ? 0 : 1;
 }
@@ -213,6 +214,7 @@ __global__ void __launch_bounds__(SV_THREADS, 3) k_verify_single(uint32_t n, con
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  if (!sc_is_canonical(k)) { verdict[i] = 1; return; }           // k >= l: its digits exceed the table
   ge_p3 Rp = double_scalar_mul(k, ge_neg(A), sw, btab, tab);
   ge_p3 d = ge_add(ld_ext(tab + 8 * EXT_WORDS), ge_neg(Rp));
   verdict[i] = ge_is_identity(ge_mul_by_cofactor(d)) ? 0 : 1;
@@ -263,6 +265,7 @@ __global__ void __launch_bounds__(64) k_verify_quad(uint32_t n, const uint8_t* _
   uint32_t k[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) k[j] = kscal[(size_t)i * 8 + j];
+  if (!sc_is_canonical(k)) { if (q == 0) verdict[i] = 1; return; }   // k >= l (whole quad leaves)
   const uint64_t kc = radix16_carries(k);
   acc = ge_identity();
   for (int j = 63; j >= 0; --j) {                  // R' = [k](-A) + [s]B: [k](-A) here

@@ -260,7 +260,9 @@ int edc_batch_verify_prehashed_fallback_device(edc_ctx* ctx, size_t n, const uin
 
 /*
  * batch::Item::verify_single (reference src/batch.rs:104-107): as edc_verify_each but with the
- * queue-time challenge k (n*32 bytes, canonical scalars) instead of the message.
+ * queue-time challenge k (n*32 bytes, canonical scalars) instead of the message. Any k >= l
+ * (which Scalar::from_hash never returns) makes the call EDC_ERR_ARG, checked on the host before
+ * anything is launched.
  */
 int edc_verify_prehashed_each(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
                               const uint8_t* k, uint8_t* verdicts);
@@ -310,8 +312,10 @@ size_t edc_keycache_size(const edc_ctx* ctx);
  * edc_batch_submit_indexed (this call does not change that list). Every later batch or per-item
  * call finds a key added here exactly as one loaded by edc_keycache_load. ok (nullable, m bytes)
  * as edc_keycache_load. The table's hash is keyed by a per-context secret, so keys taken from
- * untrusted input cannot be chosen to collide. Returns the number of distinct keys now cached or
- * <0; refused while submitted batches are in flight.
+ * untrusted input cannot be chosen to collide. Keys that do not decode (try_from's
+ * MalformedPublicKey) are NOT added (ok = 0 for them), so untrusted malformed keys cannot pin comb
+ * tables. Returns the number of distinct keys now cached or <0; refused while submitted batches
+ * are in flight.
  */
 int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok);
 

@@ -72,10 +72,16 @@ def test_no_gpu_means_loud_failure(edc):
 
 def test_prehashed_item_surface(edc):
     """batch.Item as the reference stores it ({vk_bytes, sig, k}, src/batch.rs:76-80): built from
-    the message (k hashed later, in one launch) or from k alone; neither is an error."""
+    the message (k hashed later, in one launch) or from a canonical k alone; k >= l is a ValueError."""
     vk, sig = bytes(32), bytes(64)
-    it = edc.batch.Item.prehashed(vk, sig, bytes(range(32)))
-    assert it.k == bytes(range(32)) and it._msg is None
+    k = bytes(range(31)) + b"\x0f"                      # < l
+    it = edc.batch.Item.prehashed(vk, sig, k)
+    assert it.k == k and it._msg is None
+    try:                                                # k >= l: never from Scalar::from_hash
+        edc.batch.Item.prehashed(vk, sig, bytes(range(32)))
+        raise AssertionError("expected ValueError")
+    except ValueError:
+        pass
     assert edc.batch.Item(vk, sig, b"m").k is None
     try:
         edc.batch.Item(vk, sig)

@@ -18,6 +18,7 @@ from conftest import ROOT, golden
 pytestmark = pytest.mark.gpu
 
 IDENTITY = bytes([1]) + bytes(31)
+IDENTITY_PARTIAL = bytes(32) + IDENTITY + IDENTITY + bytes(32)    # canonical X | Y | Z | T
 L_ORDER = 2**252 + 27742317777372353535851937790883648493
 BATCHES = golden("batches.json")["batches"]
 
@@ -110,8 +111,17 @@ def test_noncanonical_k_is_an_error(engine, edc):
         engine.batch_verify_prehashed(vks, sigs, k_bad, z_seed=bytes(32))
     with pytest.raises(edc.EngineError, match="canonical"):
         engine.batch_wait(engine.batch_submit_prehashed(vks, sigs, k_bad, bytes(32)))
+    # per-item path: checked on the host before any launch, including k = 2^256 - 1,
+    # whose top radix-16 digit would index past the per-item tables
+    with pytest.raises(edc.EngineError, match="canonical"):
+        engine.verify_prehashed_each(vks, sigs, k_bad)
+    with pytest.raises(edc.EngineError, match="canonical"):
+        engine.verify_prehashed_each(vks[:1], sigs[:1], [b"\xff" * 32])
+    with pytest.raises(ValueError, match="canonical"):
+        edc.batch.Item.prehashed(vks[0], sigs[0], b"\xff" * 32)
     # the context stays usable
     _check(b, *engine.batch_verify_prehashed(vks, sigs, ks, z_seed=bytes.fromhex(b["z_seed"]), want_check8=True))
+    assert engine.verify_prehashed_each(vks, sigs, ks) == b["expect_single"]
 
 
 def test_misaligned_device_pointer_is_an_error(engine):
@@ -183,10 +193,11 @@ def test_config2_prehashed_equals_message_path(engine):
 def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
     """Slot 0 (synchronous calls) decodes on a second stream beside SHA-512 / coefficients /
     binning; the pipelined slots run everything on one stream. On both: the same verdict and bad
-    flag; for batches whose points all decode (s >= l, a wrong message, valid) the same partial
-    point ([8]*P compared, partials being projective); slot 0's grouped fallback agrees with the
-    per-item kernel. (An undecodable R or key leaves an off-curve point in the MSM: its sum then
-    depends on the addition order and is not compared; the batch is rejected by its bad flag.)"""
+    flag; for batches whose points all decode (a wrong message, valid) the same partial point
+    ([8]*P compared, partials being projective); a batch rejected by its bad flag (undecodable R or
+    key, s >= l) reports the identity as its partial on every slot, byte for byte (the MSM sum of
+    an off-curve point would depend on the addition order; SURVEY §5: identical results across
+    runs); slot 0's grouped fallback agrees with the per-item kernel."""
     torch = pytest.importorskip("torch")
     import random
     dev = torch.device("cuda:0")
@@ -232,7 +243,9 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
     assert tickets == [0, 1, 2, 3]
     # partials are projective (X:Y:Z:T in the order the MSM summed): compare [8]*P compressed
     ref = engine.combine_partials([p0.raw], False)
-    if kind in ("valid", "bad_s"):      # s + l: the same scalar mod l, rejected only by the bad flag
+    if bad_flag:
+        assert p0.raw == IDENTITY_PARTIAL
+    if kind == "valid":
         assert ref == (0, IDENTITY)
     elif kind == "wrong_msg":
         assert ref[0] == 1 and ref[1] != IDENTITY
@@ -240,7 +253,9 @@ def test_dual_stream_slot0_equals_pipelined_slot(engine, kind):
         p1, f1 = ctypes.create_string_buffer(128), ctypes.c_int(0)
         assert lib.edc_batch_wait(engine.ctx, t, None, p1, ctypes.byref(f1)) == verdict
         assert f1.value == bad_flag
-        if not bad_flag or kind == "bad_s":
+        if bad_flag:
+            assert p1.raw == p0.raw
+        else:
             assert engine.combine_partials([p1.raw], False) == ref
     v = ctypes.create_string_buffer(n)
     cnt = ctypes.c_int(0)
