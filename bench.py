@@ -213,6 +213,8 @@ def main():
                          "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
     ap.add_argument("--scatter-stage", type=int, default=0,
                     help="measurement only: cap the binning scatter's LDS stage (entries; edc_debug_set_scatter_stage)")
+    ap.add_argument("--exchange-lag", type=int, default=4,
+                    help="multi-rank: partial-point exchanges (all-gathers) in flight before the oldest is combined")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -291,7 +293,20 @@ def main():
 
     pending = []
     combine = (lambda p, b: eng.combine_partials(p, b, want_check8=False))
-    allgather = sharded.torch_allgather_fn(dist, dev if backend != "gloo" else torch.device("cpu")) if dist else None
+    # multi-rank: the 129-byte records travel through a ring of asynchronous all-gathers (RCCL on the
+    # device, gloo on the host for the one-GPU rehearsals); up to --exchange-lag are in flight
+    # (RCCL: the gathered records are combined on the device right behind the collective)
+    ring = (sharded.ExchangeRing(dist, dev if backend != "gloo" else torch.device("cpu"), depth=args.exchange_lag,
+                                 device_combine=eng if backend != "gloo" else None) if dist else None)
+    xstat = {"post": 0.0, "pop": 0.0, "combine": 0.0}
+
+    def timed_ring_op(f, name):
+        def g(*a):
+            t = time.perf_counter()
+            r = f(*a)
+            xstat[name] += time.perf_counter() - t
+            return r
+        return g
 
     def submit():
         if nmb > 1:
@@ -315,22 +330,30 @@ def main():
             v = (ctypes.c_int * nmb)()
             rc = eng._check(lib.edc_batch_wait_multi(eng.ctx, pending.pop(0), nmb, v, None, None, None))
             return lambda: rc
-        if dist is None:
-            rc = eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None))
-            return lambda: rc
-        # multi-GPU: this rank's partial point of the global batch, all-gathered (RCCL) and combined
+        rc = eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None))
+        return lambda: rc
+
+    def wait_partial(t):
+        """multi-GPU: this rank's partial point of the global batch (and its reject flag)"""
         part = ctypes.create_string_buffer(128)
         bad = ctypes.c_int(0)
-        eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, part, ctypes.byref(bad)))
-        return lambda: sharded.verify_sharded(lambda zb: (part.raw, bad.value), combine, allgather, rank, world,
-                                              base)[0]
+        eng._check(lib.edc_batch_wait(eng.ctx, t, None, part, ctypes.byref(bad)))
+        return part.raw, bad.value
+
+    def submit_ticket():
+        submit()
+        return pending.pop()
 
     def run_steps(k):
         """k full batch verifications; with --inflight F, batch i+F-1 is enqueued before batch i's
-        verdict is collected (every verdict is still completed inside the loop). Multi-GPU: the
-        freed slot is refilled first, then the collected batch's partial point is all-gathered and
-        combined while the later batches run (the exchange waits for GPU time on a full device;
-        the refill must not wait behind it)."""
+        verdict is collected (every verdict is still completed inside the loop). Multi-GPU
+        (sharded.run_sharded_stream): the freed slot is refilled first, then the collected batch's
+        partial point is posted to the asynchronous all-gather ring, and the exchange --exchange-lag
+        batches back is completed and combined: no rank waits for a collective per batch."""
+        if dist is not None:
+            return sharded.run_sharded_stream(k, args.inflight, submit_ticket, wait_partial,
+                                              timed_ring_op(lambda p, b: combine(p, b)[0], "combine"), ring,
+                                              args.exchange_lag)
         codes = []
         for _ in range(k):
             done = wait_oldest() if len(pending) >= max(1, args.inflight) else None
@@ -347,23 +370,51 @@ def main():
     eng._check(lib.edc_set_msm_shape(eng.ctx, args.window_bits, args.msm_parts))
     eng._check(lib.edc_set_msm_bin_entries(eng.ctx, args.bin_entries))
     eng._check(lib.edc_reserve(eng.ctx, n))        # every in-flight slot's workspace, before any step
-    if allgather is not None:                     # communicator set-up stays out of the timed region
-        allgather(bytes(129))                     # even with --warmup 0
+    if ring is not None:                          # communicator set-up stays out of the timed region
+        ring.post(bytes(129))                     # even with --warmup 0
+        ring.pop()
+        ring.post, ring.pop = timed_ring_op(ring.post, "post"), timed_ring_op(ring.pop, "pop")
+
+    def timed(k):
+        """k steps between barriers + device syncs; the max over ranks"""
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        codes = run_steps(k)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, codes
+
     run_steps(args.warmup)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    codes = run_steps(args.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    for key in xstat:
+        xstat[key] = 0.0
+    elapsed, codes = timed(args.steps)
+    exchange_us = {key: round(v / max(1, args.steps) * 1e6, 1) for key, v in xstat.items()}
+    other = None
+    if dist and nmb == 1 and not args.prehashed:
+        # multi-rank: the other scaling shape beside the headline one, on the same ranks and data
+        # (strong: the ranks split one --n batch; weak: every rank verifies --n of its own), so a
+        # SCALE record carries both; items are a prefix of this rank's slice, z at global indices
+        n_main, base_main = n, base
+        n = args.n if args.scaling == "strong" else args.n // world
+        base = rank * n
+        eng._check(lib.edc_reserve(eng.ctx, n))
+        if n <= n_main:
+            run_steps(max(2, args.warmup))
+            el2, codes2 = timed(args.steps)
+            other = {"scaling": "weak" if args.scaling == "strong" else "strong", "sigs_per_gpu": n,
+                     "value": round(n * world * args.steps / el2, 1), "ms_per_step": round(el2 / args.steps * 1e3, 3),
+                     "verdict_ok": all(c == 0 for c in codes2)}
+        else:
+            other = {"scaling": "weak", "skipped": "the weak shape needs --n per rank; this rank holds --n / world"}
+        n, base = n_main, base_main
     verdict_ok = all(c == 0 for c in codes)
     # an A/B build (--lib, tools/ab_variants.sh) may be a timing probe that is wrong by design:
     # report its verdicts instead of stopping; the product library must verify the batch
@@ -470,6 +521,14 @@ def main():
                        "prehashed": bool(args.prehashed), "batches_per_launch": nmb,
                        "multi_union_first": bool(nmb > 1 and not args.multi_exact),
                        "parallelism": f"shard{world}" if world > 1 else "single"},
+            # the process group the ranks actually formed (None: one process, no collectives)
+            "comm": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                      "exchange_lag": args.exchange_lag,
+                      "exchange_us": exchange_us,
+                      "exchange_note": "host time per batch inside the timed loop: posting the all-gather, "
+                                       "completing it (waits for the collective), combining the partials"}
+                     if dist else None),
+            "scaling_other_shape": other,
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),

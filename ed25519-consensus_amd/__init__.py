@@ -51,7 +51,7 @@ ABI_SYMBOLS = [
     "edc_batch_verify_prehashed", "edc_batch_verify_prehashed_device", "edc_batch_submit_prehashed",
     "edc_batch_submit_prehashed_device", "edc_batch_verify_prehashed_fallback",
     "edc_batch_verify_prehashed_fallback_device", "edc_multi_route", "edc_multi_debug_force_staged",
-    "edc_batch_submit_multi_device", "edc_batch_wait_multi",
+    "edc_batch_submit_multi_device", "edc_batch_wait_multi", "edc_combine_records_device",
 ]
 
 
@@ -110,6 +110,7 @@ def load_library(path=None):
         lib.edc_batch_partial_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                  c_vp, ctypes.POINTER(ctypes.c_int)]
         lib.edc_combine_partials.argtypes = [c_vp, c_sz, c_u8p, ctypes.c_int, c_vp]
+        lib.edc_combine_records_device.argtypes = [c_vp, c_vp, c_sz, c_vp, c_sz, c_vp]
         lib.edc_batch_submit_device.restype = ctypes.c_int64
         lib.edc_batch_submit_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                 ctypes.c_int]
@@ -499,6 +500,12 @@ class Engine:
         with self._lock:
             self._check(self.lib.edc_sign(self.ctx, n, b"".join(seeds), len(seeds), idx, arena, offs, vk, sig))
         return [vk.raw[32 * i:32 * i + 32] for i in range(n)], [sig.raw[64 * i:64 * i + 64] for i in range(n)]
+
+    def combine_records_device(self, stream, g, d_records, stride, d_out):
+        """Enqueue the combine of g gathered 129-byte exchange records (device memory) on `stream`
+        (a raw HIP stream handle); the 256-byte result block lands in d_out (device)."""
+        self._check(self.lib.edc_combine_records_device(self.ctx, ctypes.c_void_p(stream), g, ctypes.c_void_p(d_records),
+                                                        stride, ctypes.c_void_p(d_out)))
 
     def combine_partials(self, partials, bad_any, want_check8=True):
         check8 = ctypes.create_string_buffer(32) if want_check8 else None

@@ -686,7 +686,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   // Contract while st2 runs (between ev_keys and the wait on ev_dec below): k_decompress reads
   // d_sig, d_vk, key_rep, flags[FLAG_NKEYS / FLAG_OVF] and the key cache, and writes pts,
   // itembad + cap_n, keybad and flags[FLAG_BAD / FLAG_UNCACHED] (atomics). The kernels enqueued on
-  // st in between (challenge, coefficients, binning) must not read pts / keybad / itembad + cap_n,
+  // st in between (challenge, coefficients, binning, bucket sort) must not read pts / keybad / itembad + cap_n,
   // write key_rep or FLAG_NKEYS / FLAG_OVF, or plain-store into flags; anything that does must
   // come after the ev_dec wait. tests/test_gpu_prehashed.py compares slot 0 (dual stream) with a
   // pipelined slot (one stream) on batches that fail in the decode and in the s check.
@@ -708,6 +708,10 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   if (with_bin && EDC_RUN(8))
     launch_msm_bin(st, *P, batch_terms(*P, s, N, split), split ? 2 + 3 * N : 1 + 2 * N, s.counts, s.offsets, s.cursor,
                    s.entries, s.flags, true);
+  // the per-bin bucket sort needs only the binning: before the decode join, so on the dual-stream
+  // slot it runs beside the decode instead of after it
+  if (with_bin && EDC_RUN(256))
+    launch_msm_sort(st, *P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.buckets);
   // the points are decoded last, right before the accumulation gathers them, so the freshly
   // written point table (134 MB at 2^20) is still in the Infinity Cache for the random row gathers
   mark(PH_DECOMP);
@@ -849,6 +853,7 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
                     s.itembad, s.flags, s.mb_xpt, s.mb_xrg, s.mb_xscal);
   const MsmTerms terms{n, (uint32_t)n_per, 0u, nb, 1u, s.scal, s.mb_xpt, s.mb_xrg, s.mb_xscal, 0u, per_sig ? 3u : 1u};
   launch_msm_bin(st, P, terms, (uint32_t)(N + full_max), s.counts, s.offsets, s.cursor, s.entries, s.flags, true);
+  launch_msm_sort(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.buckets);
   if (dual) CK(hipStreamWaitEvent(st, s.ev_dec, 0));
   else
     launch_decompress(st, n, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
@@ -1284,6 +1289,16 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
   return combine_points(ctx, g, partials, bad_any, check8, nullptr);
 }
 
+int edc_combine_records_device(edc_ctx* ctx, void* stream, size_t g, const uint8_t* d_records, size_t stride,
+                               uint8_t* d_out) {
+  if (!ctx || !d_out || (g && !d_records) || stride < 129 || g > 4096) return EDC_ERR_ARG;
+  if (!aligned16(d_out)) { ctx->err = "d_out must be 16-byte aligned"; return EDC_ERR_ARG; }
+  CK(hipSetDevice(ctx->device));
+  launch_combine_records(reinterpret_cast<hipStream_t>(stream), (uint32_t)g, d_records, (uint32_t)stride, d_out);
+  CK(hipGetLastError());
+  return 0;
+}
+
 int edc_challenge(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                   const uint64_t* msg_off, uint8_t* k_out) {
   if (!ctx || (n && !k_out)) return EDC_ERR_ARG;
@@ -1472,6 +1487,7 @@ static int fallback_ranges(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk,
   const MsmTerms terms{(uint32_t)n, (uint32_t)rsize, npoint, (uint32_t)nx, 1, s.scal, ctx->fb_xpt, ctx->fb_xrg,
                        ctx->fb_xscal};
   launch_msm_bin(st, P, terms, npoint + (uint32_t)nx, s.counts, s.offsets, s.cursor, s.entries, s.flags);
+  launch_msm_sort(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.buckets);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
                     s.slice_T);
   launch_msm_range_tail(st, P, s.slice_W, s.slice_T, s.win, ctx->fb_rv);

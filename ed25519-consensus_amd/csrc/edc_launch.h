@@ -54,6 +54,11 @@ hipError_t msm_init_device();
 // edc_msm.hip (counts_zeroed: the caller already cleared counts, e.g. launch_init_batch)
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed = false);
+// per-bin counting sort of the binned entries by bucket (needs only the binning: enqueued right
+// after launch_msm_bin, so on a dual-stream slot it overlaps the decode)
+void launch_msm_sort(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
+                     const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, uint32_t* buckets);
+// accumulation (+ bin reduction) of the sorted entries; launch_msm_sort must have run
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip = 0,
@@ -68,6 +73,7 @@ void launch_msm_range_tail(hipStream_t st, const MsmPlan& P, const uint32_t* sli
 void launch_msm_multi_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                            uint32_t* win, const int* flags, const uint8_t* rbad, int want_compress, uint8_t* out,
                            uint8_t* hout);
+void launch_combine_records(hipStream_t st, uint32_t g, const uint8_t* recs, uint32_t stride, uint8_t* out);
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,
                     uint8_t* out);
 // 256-byte result block src -> dst (dst may be a peer device's memory)

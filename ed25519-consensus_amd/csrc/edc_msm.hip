@@ -423,6 +423,13 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
 #ifndef EDC_ACC_OCC
 #define EDC_ACC_OCC 4
 #endif
+// 1: the accumulation workgroup reduces its own bin after the heads merge (weighted_sum_256 over
+// the 256 bucket sums, in the LDS the row buffers used), so no separate reduction kernel runs
+#ifndef EDC_FUSED_REDUCE
+#define EDC_FUSED_REDUCE 0
+#endif
+constexpr int ACC_LDS_WORDS = EDC_FUSED_REDUCE && NSLICE * EXT_WORDS > 4 * WAVE_ROWS_WORDS ? NSLICE * EXT_WORDS
+                                                                                             : 4 * WAVE_ROWS_WORDS;
 #ifndef EDC_ACC_HOIST
 #define EDC_ACC_HOIST 0   // measurement knob: let the compiler hoist the DMA piece map (needs VGPRs)
 #endif
@@ -442,7 +449,7 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
 #ifndef EDC_ACC_LDS_PAD
 #define EDC_ACC_LDS_PAD 0   // measurement knob: extra LDS words per workgroup (caps workgroups per CU)
 #endif
-  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS + EDC_ACC_LDS_PAD];   // row buffers of the 4 waves
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[ACC_LDS_WORDS + EDC_ACC_LDS_PAD];   // row buffers of the 4 waves
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;
@@ -547,6 +554,24 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
     st_ext(bucket_slot(buckets, bin, cb), acc);
   }
   ACC_STAMP(3, __builtin_amdgcn_s_memtime());
+#if EDC_FUSED_REDUCE
+  // the bin's reduction, W = sum_t (t+1) S_t and T = sum_t S_t (k_msm_reduce_quad's weighted sum):
+  // every bucket sum is final in `buckets` after the barrier (the same workgroup wrote them, as the
+  // heads above); staged into the LDS the row buffers used
+  __threadfence_block();
+  __syncthreads();
+  st_ext(lbuf + t * EXT_WORDS, ld_ext(bucket_slot(buckets, bin, t)));
+  __syncthreads();
+  ge_p3 ws, tot;
+  weighted_sum_256(lbuf, lbuf, lbuf + 64 * EXT_WORDS, ws, tot);
+  if (t < 4) {
+    const ge_p3 W = quad_add(ws, tot);              // sum_t (t + 1) S_t
+    if (t == 0) {
+      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
+      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
+    }
+  }
+#endif
   ACC_STAMP(6, __builtin_amdgcn_s_memrealtime());
 }
 
@@ -948,6 +973,21 @@ __global__ void k_combine_blocks(uint32_t g, const uint8_t* __restrict__ blocks,
   finish_point(acc, bad, want_compress, out);
 }
 
+// combine g exchange records (stride bytes apart: canonical 128-byte partial, then the bad byte),
+// as the multi-rank all-gather leaves them in device memory
+__global__ void k_combine_records(uint32_t g, const uint8_t* __restrict__ recs, uint32_t stride,
+                                  uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 acc = ge_identity();
+  int bad = 0;
+  for (uint32_t i = 0; i < g; ++i) {
+    acc = ge_add(acc, ext_from_canonical_bytes(recs + (size_t)stride * i));
+    bad |= recs[(size_t)stride * i + 128] ? 1 : 0;
+  }
+  for (int j = 0; j < 64; ++j) reinterpret_cast<int*>(out)[j] = 0;
+  finish_point(acc, bad, 0, out);
+}
+
 // one shard's 256-byte result block to the first device's gather buffer (a peer store over xGMI
 // when the devices differ): a kernel on the shard's stream, so the copy stays asynchronous
 __global__ void k_copy_block(const uint4* __restrict__ src, uint4* __restrict__ dst) {
@@ -1011,21 +1051,23 @@ hipError_t msm_init_device() {
 
 static const size_t kReduceLds = (size_t)NSLICE * EXT_WORDS * sizeof(uint32_t);  // 256 points; scans reuse them
 
+void launch_msm_sort(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
+                     const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, uint32_t* buckets) {
+  hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end, buckets);
+}
+
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip,
                        hipEvent_t acc_begin, hipEvent_t acc_end) {
-  // one workgroup per bin (sort, then accumulation), then the lane-parallel bin reductions
-  // (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
-  if (!(probe_skip & 256))
-    hipLaunchKernelGGL(k_msm_sort, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, entries, sorted, bucket_end,
-                       buckets);
+  // one workgroup per bin (accumulation of the entries k_msm_sort ordered), then the bin
+  // reductions (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
   if (acc_begin) (void)hipEventRecord(acc_begin, st);      // timed batches: the accumulation alone
   if (!(probe_skip & 32))
     hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
                        buckets, heads, slice_W, slice_T);
   if (acc_end) (void)hipEventRecord(acc_end, st);
-  if (probe_skip & 64) return;
+  if ((probe_skip & 64) || EDC_FUSED_REDUCE) return;
   if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
   else if (P.nbin() < REDUCE64_MAX_BINS)
@@ -1091,6 +1133,10 @@ void launch_copy_block(hipStream_t st, const uint8_t* src, uint8_t* dst) {
 
 void launch_combine_blocks(hipStream_t st, uint32_t g, const uint8_t* blocks, int want_compress, uint8_t* out) {
   hipLaunchKernelGGL(k_combine_blocks, dim3(1), dim3(64), 0, st, g, blocks, want_compress, out);
+}
+
+void launch_combine_records(hipStream_t st, uint32_t g, const uint8_t* recs, uint32_t stride, uint8_t* out) {
+  hipLaunchKernelGGL(k_combine_records, dim3(1), dim3(64), 0, st, g, recs, stride, out);
 }
 
 void launch_combine(hipStream_t st, uint32_t g, const uint8_t* partials, int bad, int want_compress,

@@ -77,6 +77,130 @@ def torch_allgather_fn(dist, device):
     return fn
 
 
+class ExchangeRing:
+    """Pipelined exchange of one fixed-size record per rank and batch (the 129-byte partial +
+    reject flag), with up to `depth` exchanges in flight: post() starts the all-gather of a batch
+    and returns at once, pop() completes the OLDEST one and returns its per-rank records (rank
+    order). Every rank posts its batches in the same order, so collective i matches batch i on all
+    ranks; the verdicts still complete in queue order.
+
+    On a GPU device (RCCL) the staging copies and the collective run on a private non-blocking
+    torch stream: the host never waits for the collective inside post(), and the engine's slot
+    streams (blocking streams, hipExtStreamCreateWithCUMask takes no flags) never wait behind it.
+    Each in-flight exchange owns its pinned host and device buffers, reused only after pop().
+    On the CPU (gloo) the collective is async_op=True and pop() waits for its work handle.
+
+    device_combine (GPU only): an Engine. The combine of the gathered records is then enqueued on
+    the same side stream right behind the collective (edc_combine_records_device: sum, x8,
+    identity test on the device, no host round trip of the records), and pop() returns the
+    verdict code instead of the records (`combines` is True)."""
+
+    def __init__(self, dist, device, rec_len=129, depth=4, device_combine=None):
+        import torch
+        self.dist, self.n = dist, rec_len
+        self.world = dist.get_world_size()
+        self.gpu = device.type != "cpu"
+        self.eng = device_combine if self.gpu else None
+        self.combines = self.eng is not None
+        self.q = []
+        nbuf = depth + 1
+        if self.gpu:
+            self.side = torch.cuda.Stream(device=device)
+            nres = 256 if self.combines else self.world * rec_len      # result block / the records
+            with torch.cuda.stream(self.side):
+                self.bufs = [(torch.empty(rec_len, dtype=torch.uint8, pin_memory=True),
+                              torch.empty(nres, dtype=torch.uint8, pin_memory=True),
+                              torch.empty(rec_len, dtype=torch.uint8, device=device),
+                              torch.empty(self.world * rec_len, dtype=torch.uint8, device=device),
+                              torch.empty(256, dtype=torch.uint8, device=device))
+                             for _ in range(nbuf)]
+        else:
+            self.bufs = [(torch.empty(rec_len, dtype=torch.uint8), torch.empty(self.world * rec_len, dtype=torch.uint8))
+                         for _ in range(nbuf)]
+        self.free = list(range(nbuf))
+
+    def __len__(self):
+        return len(self.q)
+
+    def post(self, rec):
+        import numpy as np
+        import torch
+        assert len(rec) == self.n
+        if not self.free:
+            raise RuntimeError("ExchangeRing: more exchanges in flight than its depth; pop() first")
+        i = self.free.pop()
+        if self.gpu:
+            h_in, h_out, d_in, d_out, d_res = self.bufs[i]
+            with torch.cuda.stream(self.side):
+                h_in.numpy()[:] = np.frombuffer(rec, dtype=np.uint8)
+                d_in.copy_(h_in, non_blocking=True)
+                work = self.dist.all_gather_into_tensor(d_out, d_in, async_op=True)
+                work.wait()              # the side stream waits for the collective; the host does not
+                if self.combines:
+                    self.eng.combine_records_device(self.side.cuda_stream, self.world, d_out.data_ptr(), self.n,
+                                                    d_res.data_ptr())
+                    h_out.copy_(d_res, non_blocking=True)
+                else:
+                    h_out.copy_(d_out, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self.q.append((i, ev))
+        else:
+            t_in, t_out = self.bufs[i]
+            t_in.numpy()[:] = np.frombuffer(rec, dtype=np.uint8)
+            self.q.append((i, self.dist.all_gather_into_tensor(t_out, t_in, async_op=True)))
+
+    def pop(self):
+        i, h = self.q.pop(0)
+        if self.gpu:
+            h.synchronize()
+        else:
+            h.wait()
+        host = self.bufs[i][1].numpy().tobytes()
+        self.free.append(i)
+        if self.combines:                # the device's verdict word: 0 Ok, 1 reject
+            return int.from_bytes(host[:4], "little")
+        return [host[r * self.n:(r + 1) * self.n] for r in range(self.world)]
+
+
+def run_sharded_stream(k, inflight, submit_fn, wait_fn, combine_fn, ring, lag):
+    """bench.py's multi-rank loop: k consecutive batches of this rank's shard, `inflight` of them
+    submitted ahead on the device and `lag` exchanges in flight. When the oldest batch is
+    collected, the freed slot is refilled first (the device stays full), then the batch's record
+    is posted to the ring, and exchanges older than `lag` are completed and combined. Returns the
+    verdict codes in batch order.
+
+    submit_fn() -> ticket                     enqueue the next batch of this rank's shard
+    wait_fn(ticket) -> (partial_128, bad)     its partial point and early-reject flag
+    combine_fn(partials, bad_any) -> code     [8]*sum == identity over the ranks' partials
+    """
+    pending, codes = [], []
+
+    def finish():
+        res = ring.pop()
+        if getattr(ring, "combines", False):         # combined on the device behind the collective
+            codes.append(res)
+        else:
+            codes.append(combine_fn([r[:128] for r in res], any(r[128] for r in res)))
+
+    def post(res):
+        part, bad = res
+        ring.post(bytes(part) + bytes([1 if bad else 0]))
+        while len(ring) > lag:
+            finish()
+
+    for _ in range(k):
+        res = wait_fn(pending.pop(0)) if len(pending) >= max(1, inflight) else None
+        pending.append(submit_fn())
+        if res is not None:
+            post(res)
+    while pending:
+        post(wait_fn(pending.pop(0)))
+    while len(ring):
+        finish()
+    return codes
+
+
 def find_invalid_sharded(shard_ok_fn, find_fn, allgather_obj_fn, rank, world, lo):
     """Multi-GPU fallback after a failed global batch (the caller's verify_single loop
     of reference tests/batch.rs:37-43). Every shard's own partial satisfies [8]P_g == 0 when all of

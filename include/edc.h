@@ -168,6 +168,17 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
                          uint8_t check8[32]);
 
 /*
+ * Device-side combine of g gathered exchange records (the multi-rank path's all-gather output,
+ * already in this GPU's memory): record r at d_records + r*stride holds a shard's canonical
+ * 128-byte partial point followed by its bad byte. The sum, x8 and the identity test (reference
+ * src/batch.rs:212-216) run as one small kernel ENQUEUED on the caller's HIP stream `stream`
+ * (the stream the all-gather ran on, so no host round trip and no synchronization); the 256-byte
+ * result block lands in d_out (device, 16-byte aligned): int[0] = 0 Ok / 1 reject, int[1] = bad.
+ */
+int edc_combine_records_device(edc_ctx* ctx, void* stream, size_t g, const uint8_t* d_records, size_t stride,
+                               uint8_t* d_out);
+
+/*
  * VerificationKey::try_from(vk) + VerificationKey::verify(sig, msg) for each item
  *   reference src/verification_key.rs:160-175 (try_from -> MalformedPublicKey)
  *             src/verification_key.rs:225-258 (verify / verify_prehashed)

@@ -98,3 +98,53 @@ def test_config2_valid_batch_vs_oracle(edc):
     gpu, (code, c8) = _run(edc, torch, "c3", lambda *a: None)
     assert (code, c8) == (0, IDENTITY)
     assert gpu[0] == gpu[1] == (0, IDENTITY)
+
+
+def test_config1_failing_batch_vs_oracle(edc):
+    """configs[1]: 2^16 signatures with distinct keys and 32-byte messages, one corrupted s: the
+    non-identity [8]*check of both plans (grouped first batch, per-signature second) against the
+    oracle."""
+    torch = pytest.importorskip("torch")
+
+    def corrupt(vk, sig, msg, off):
+        sig[64 * 40_000 + 37] ^= 0x02         # s changed, still canonical
+
+    gpu, (code, c8) = _run(edc, torch, "c2", corrupt)
+    assert code == 1 and c8 is not None and c8 != IDENTITY
+    assert gpu[0] == gpu[1] == (1, c8)
+
+
+def test_config3_failing_batch_vs_oracle(edc):
+    """configs[3]: 2^20 votes with the 196-case ZIP215 corpus (small-order and non-canonical A / R,
+    reference tests/small_order.rs:12-77) at seeded positions and one signature over another
+    message: the failing batch's non-identity [8]*check against the oracle, byte for byte (the
+    corpus points are torsion points, so this pins their MSM terms at full size too)."""
+    torch = pytest.importorskip("torch")
+    from conftest import golden
+    sys.path.insert(0, ROOT)
+    import bench
+    oc = _oracle_c()
+    dev = torch.device("cuda:0")
+    fx = golden("zip215_small_order.json")
+    eng = edc.Engine(0)
+    try:
+        vk, sig, msg, off, expect, cpos = bench.make_c4_workload(sys.modules["ed25519_consensus_amd"], eng, torch, dev,
+                                                                 1 << 20, 150, 120, fx["cases"],
+                                                                 bytes.fromhex(fx["msg"]))
+        torch.cuda.synchronize()
+        n = 1 << 20
+        zseed = bytes([0x3D]) * 32
+        gpu = []
+        for _ in range(2):
+            c8 = ctypes.create_string_buffer(32)
+            code = eng.lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                                   off.data_ptr(), zseed, 0, None, c8)
+            gpu.append((code, c8.raw))
+        hv, hs, hm, ho = _host(vk, sig, msg, off)
+        code, c8, secs = oc.batch_verify_parallel(hv, hs, hm, ho, zseed)
+        print(f"\n[fullsize-oracle] configs[3] n={n}: oracle {secs:.2f} s on {oc.host_threads()} host threads; "
+              f"gpu {gpu[0][0]} / {gpu[1][0]}, oracle {code}, check8 {c8.hex() if c8 else None}")
+        assert code == 1 and c8 is not None and c8 != IDENTITY
+        assert gpu[0] == gpu[1] == (1, c8)
+    finally:
+        eng.close()

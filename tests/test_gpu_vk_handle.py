@@ -53,6 +53,9 @@ def test_try_from_malformed_key(cached, edc):
             edc.VerificationKey.try_from(enc, cached)
     got = edc.VerificationKey.try_from_many(bad[:4] + [bad[0]], cached, keep_decoded=True)
     assert all(isinstance(g, edc.MalformedPublicKey) for g in got)
+    assert cached.keycache_size() == 0                  # malformed keys never enter the cache
+    n0, ok = cached.keycache_add(bad[:4])
+    assert n0 == 0 and not any(ok)
 
 
 def test_zip215_corpus_with_decoded_keys(cached, edc):
@@ -86,7 +89,8 @@ def test_golden_batches_after_incremental_add(cached, b):
         assert code == b["expect_code"], b["name"]
         if b["expect_check8"] is not None:
             assert check8.hex() == b["expect_check8"], b["name"]
-    assert cached.keycache_size() == len(distinct)
+    # keys that do not decode are not added (edc_keycache_add): the cache holds the decodable ones
+    assert cached.keycache_size() == sum(1 for c in cached.vk_validate(distinct) if c == 0)
     assert cached.verify_each(vks, sigs, msgs) == b["expect_single"]
 
 

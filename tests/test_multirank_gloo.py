@@ -1,6 +1,7 @@
-"""CPU, world_size 2 over gloo: the multi-GPU orchestration of bench.py / sharded.py --
+"""CPU, world_size 2 / 4 / 8 over gloo: the multi-GPU orchestration of bench.py / sharded.py --
 contiguous queue slices, global z offsets, a 129-byte all-gather per rank and the combine --
-reproduces the unsharded verdict and [8]*check. The per-rank partial is computed by the C
+reproduces the unsharded verdict and [8]*check, one batch at a time and as bench.py's pipelined
+stream (asynchronous exchange ring, several batches and all-gathers in flight). The per-rank partial is computed by the C
 oracle here (no GPU); on MI355X the same driver calls edc_batch_partial_device and RCCL."""
 import json
 import os
@@ -66,6 +67,70 @@ def test_two_rank_sharded_verify(tmp_path, name, world):
         res = json.load(open(out + f".{r}"))
         assert res["code"] == b["expect_code"]
         assert res["check8"] == b["expect_check8"]
+
+
+STREAM = ["mixed_corpus_one_bad", "repeated_keys_varlen", "undecodable_R", "batch_verify_32", "two_bad_of_300",
+          "repeated_keys_varlen", "mixed_corpus_one_bad"]
+
+
+def _stream_worker(rank, world, port, inflight, lag, out_path):
+    """bench.py's multi-rank loop (sharded.run_sharded_stream + ExchangeRing over gloo): a stream of
+    golden batches, `inflight` submitted ahead, `lag` all-gathers in flight; the oracle computes
+    each rank's partial where the GPU runs edc_batch_wait(partial)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_c
+    from conftest import load_pkg
+    load_pkg()
+    from importlib import import_module
+    sharded = import_module("ed25519_consensus_amd.sharded")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gold = {x["name"]: x for x in golden("batches.json")["batches"]}
+    submitted, log = [], []
+
+    def submit():
+        j = len(submitted)
+        submitted.append(j)
+        log.append(("submit", j))
+        return j
+
+    def wait(j):
+        b = gold[STREAM[j]]
+        items = [(bytes.fromhex(v), bytes.fromhex(s), bytes.fromhex(m)) for v, s, m in b["items"]]
+        lo, hi = sharded.shard_bounds(len(items), world)[rank]
+        part, bad = oracle_c.shard_partial_affine(items[lo:hi], bytes.fromhex(b["z_seed"]), lo)
+        log.append(("wait", j))
+        return part + bytes(64), bad
+
+    def combine(parts, bad_any):
+        code, _ = oracle_c.combine_affine([p[:64] for p in parts])
+        return 1 if bad_any else code
+
+    ring = sharded.ExchangeRing(dist, torch.device("cpu"), depth=lag)
+    codes = sharded.run_sharded_stream(len(STREAM), inflight, submit, wait, combine, ring, lag)
+    with open(out_path + f".{rank}", "w") as f:
+        json.dump({"codes": codes, "log": log}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,inflight,lag", [(2, 1, 1), (4, 3, 2), (8, 4, 3)])
+def test_stream_loop_in_order(tmp_path, world, inflight, lag):
+    """The multi-rank loop of bench.py at 2 / 4 / 8 ranks with several batches and exchanges in
+    flight: every rank gets every batch's unsharded verdict, in batch order; a batch is submitted
+    up to `inflight` ahead of its collection (the refill precedes the exchange)."""
+    out = str(tmp_path / "stream")
+    mp.start_processes(_stream_worker, args=(world, _free_port(), inflight, lag, out), nprocs=world, join=True,
+                       start_method="spawn")
+    gold = {x["name"]: x for x in golden("batches.json")["batches"]}
+    expect = [gold[nm]["expect_code"] for nm in STREAM]
+    for r in range(world):
+        res = json.load(open(out + f".{r}"))
+        assert res["codes"] == expect
+        first_wait = [i for i, (op, _) in enumerate(res["log"]) if op == "wait"][0]
+        assert [j for op, j in res["log"][:first_wait] if op == "submit"] == list(range(inflight))
 
 
 def _fallback_worker(rank, world, port, name, out_path):

@@ -17,6 +17,8 @@
 #   pmc              tools/pmc_passes.sh (VALU / INT / FETCH / WRITE passes; then tools/pmc_summary.py here)
 #   rccl1            forced single-rank RCCL loop (process group + per-batch all-gather)
 #   gloo2            two ranks sharing the GPU over gloo, weak and strong
+#   lat | lat=<v>    tools/latency_probe.py (one synchronous batch at a time) on the product / a variant build
+#   gloo4            four ranks sharing the GPU over gloo (weak, with the strong shape beside it)
 #   ab=<v1,v2,..>    alternating A/B of variant builds csrc/libedc_<v>.so ("base" = libedc.so) on
 #                    AB_CONFIGS (default "c3 n17 c2 c5"), AB_REPS rounds (default 2)
 #   bench=<args>     one bench.py run with these arguments (commas for spaces)
@@ -85,6 +87,9 @@ for step in "$@"; do
     gloo2)
       run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
       run gloo2_strong 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --scaling strong --steps 20 --warmup 3 --no-cpu-baseline ;;
+    lat) run lat 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 ;;
+    lat=*) v=${step#lat=}; run lat_$v 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 --lib "$PWD/$D/libedc_$v.so" ;;
+    gloo4) run gloo4 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 4 --steps 20 --warmup 3 --no-cpu-baseline ;;
     ab=*)
       IFS=, read -ra libs <<< "${step#ab=}"
       for rep in $(seq 1 "${AB_REPS:-2}"); do

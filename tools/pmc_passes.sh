@@ -8,10 +8,9 @@ mkdir -p gpurun_out
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --profile-steps 1 > gpurun_out/pmc_$name.log 2>&1
+    python3 bench.py --steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --profile-steps 1 $BENCH_ARGS > gpurun_out/pmc_$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"; return $rc
 }
 run valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE &&
 run int SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SALU SQ_INSTS_LDS &&
-run fetch FETCH_SIZE &&
-run write WRITE_SIZE
+[ -n "$VALU_ONLY" ] || { run fetch FETCH_SIZE && run write WRITE_SIZE; }
