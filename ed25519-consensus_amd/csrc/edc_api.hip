@@ -686,11 +686,17 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   // Contract while st2 runs (between ev_keys and the wait on ev_dec below): k_decompress reads
   // d_sig, d_vk, key_rep, flags[FLAG_NKEYS / FLAG_OVF] and the key cache, and writes pts,
   // itembad + cap_n, keybad and flags[FLAG_BAD / FLAG_UNCACHED] (atomics). The kernels enqueued on
-  // st in between (challenge, coefficients, binning, bucket sort) must not read pts / keybad / itembad + cap_n,
+  // st in between (coefficients, binning, bucket sort) must not read pts / keybad / itembad + cap_n,
   // write key_rep or FLAG_NKEYS / FLAG_OVF, or plain-store into flags; anything that does must
   // come after the ev_dec wait. tests/test_gpu_prehashed.py compares slot 0 (dual stream) with a
   // pipelined slot (one stream) on batches that fail in the decode and in the s check.
+  // The decode is released after SHA-512, not right after the key grouping: both are VALU-bound,
+  // and a decode launched first fills the GPU and starves SHA-512 (measured: the challenge took
+  // ~1.0 ms beside the decode instead of 0.22 ms alone), so the light coefficient / binning /
+  // sort chain queued behind SHA-512 ran after the decode instead of beside it.
   const bool dual = EDC_DUAL_STREAM && s.st2 && !s.timed;
+  mark(PH_CHALLENGE);
+  if (!d_k && EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   if (dual) {
     CK(hipEventRecord(s.ev_keys, st));
     CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
@@ -699,8 +705,6 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
                         ctx->kc(), split);
     CK(hipEventRecord(s.ev_dec, s.st2));
   }
-  mark(PH_CHALLENGE);
-  if (!d_k && EDC_RUN(2)) launch_challenge(st, N, d_vk, d_sig, d_msg, d_off, s.k);
   mark(PH_COEF);
   if (EDC_RUN(4)) launch_coef(st, N, d_sig, s.kin, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
               per_sig, s.coef_part, split);
@@ -726,7 +730,8 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
 // Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
 static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                          const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
-                         const uint8_t* d_z, int want_compress, const uint32_t* d_k = nullptr) {
+                         const uint8_t* d_z, int want_compress, const uint32_t* d_k = nullptr,
+                         bool latency = false) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   int rc = ensure_slot(ctx, s, n);
   if (rc) return rc;
@@ -740,7 +745,7 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
                     s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0, s.timed ? s.ev_acc[0] : nullptr,
-                    s.timed ? s.ev_acc[1] : nullptr);
+                    s.timed ? s.ev_acc[1] : nullptr, latency);
   s.acc_nbin = P.nbin();
   if (s.timed) {   // the accumulation's entry count, read at the wait without another sync
     CK(hipMemcpyAsync(s.h_acc, s.offsets + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -840,7 +845,8 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
     launch_keys(st, n, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
                 s.key_index, s.key_acc, s.flags, kstride);
   }
-  const bool dual = EDC_DUAL_STREAM && s.st2;       // same contract as enqueue_prefix
+  const bool dual = EDC_DUAL_STREAM && s.st2;       // same contract (and order) as enqueue_prefix
+  if (!d_k) launch_challenge(st, n, d_vk, d_sig, d_msg, d_off, s.k);
   if (dual) {
     CK(hipEventRecord(s.ev_keys, st));
     CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
@@ -848,7 +854,6 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
                       false);
     CK(hipEventRecord(s.ev_dec, s.st2));
   }
-  if (!d_k) launch_challenge(st, n, d_vk, d_sig, d_msg, d_off, s.k);
   launch_multi_coef(st, n, nb, kstride, per_sig, d_sig, s.kin, seed, z_base, s.key_index, s.scal, s.mb_acc, s.u_acc,
                     s.itembad, s.flags, s.mb_xpt, s.mb_xrg, s.mb_xscal);
   const MsmTerms terms{n, (uint32_t)n_per, 0u, nb, 1u, s.scal, s.mb_xpt, s.mb_xrg, s.mb_xscal, 0u, per_sig ? 3u : 1u};
@@ -994,7 +999,9 @@ static int run_batch_sync(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uin
                           uint8_t check8[32], uint8_t partial[128], int* bad, const uint32_t* d_k = nullptr) {
   Slot& s = ctx->slot[0];
   if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
-  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, check8 != nullptr, d_k);
+  // a synchronous call is one batch on an otherwise idle GPU: latency-shaped kernels (see
+  // launch_msm_bucket); pipelined submissions keep the work-minimal ones
+  int rc = enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, check8 != nullptr, d_k, true);
   if (rc) return rc;
   return finish_batch(ctx, s, check8, partial, bad);
 }

@@ -62,7 +62,7 @@ void launch_msm_sort(hipStream_t st, const MsmPlan& P, const uint32_t* counts, c
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip = 0,
-                       hipEvent_t acc_begin = nullptr, hipEvent_t acc_end = nullptr);
+                       hipEvent_t acc_begin = nullptr, hipEvent_t acc_end = nullptr, bool latency = false);
 size_t msm_bucket_words(uint32_t nbin);
 void launch_msm_tail(hipStream_t st, const MsmPlan& P, const uint32_t* slice_W, const uint32_t* slice_T,
                      uint32_t* win, int* flags, int want_compress, uint8_t* out, uint8_t* hout = nullptr);

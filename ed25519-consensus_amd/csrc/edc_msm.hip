@@ -644,6 +644,13 @@ __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_
 // additions of 2 multiplication rounds each, instead of ~20 one-lane additions of 9 rounds).
 // About 4x the instructions of k_msm_reduce, so large batches keep the lane-parallel form.
 constexpr uint32_t REDUCE_QUAD_MAX_BINS = 128;
+// synchronous calls: up to what one round of k_msm_reduce_quad workgroups holds (143 VGPRs: 3
+// per CU, 768 on 256 CUs); past it a second round costs more than the lane-parallel form (measured:
+// configs[2]'s 1,040 bins 1.83 vs 1.79 ms per call, 2^17's 592 bins 0.54 vs 0.56 ms, profiles/r05)
+#ifndef EDC_REDUCE_QUAD_LATENCY_MAX_BINS
+#define EDC_REDUCE_QUAD_LATENCY_MAX_BINS 768u
+#endif
+constexpr uint32_t REDUCE_QUAD_LATENCY_MAX_BINS = EDC_REDUCE_QUAD_LATENCY_MAX_BINS;
 #ifndef EDC_REDUCE64_MAX_BINS
 #define EDC_REDUCE64_MAX_BINS 256
 #endif
@@ -1040,6 +1047,10 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
   }
   hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
+#ifdef EDC_PROBE_EXTRA_SCANS   // measurement only: N more (idempotent) dependent launches per batch
+  for (int r = 0; r < EDC_PROBE_EXTRA_SCANS; ++r)
+    hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
+#endif
   hipLaunchKernelGGL(k_msm_scatter, dim3(sgrid), dim3(SCATTER_THREADS), bins_bytes + (size_t)stage_cap * sizeof(uint2), st, P, T,
                      SB, cursor, entries, flags, stage_cap);
 }
@@ -1059,7 +1070,7 @@ void launch_msm_sort(hipStream_t st, const MsmPlan& P, const uint32_t* counts, c
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip,
-                       hipEvent_t acc_begin, hipEvent_t acc_end) {
+                       hipEvent_t acc_begin, hipEvent_t acc_end, bool latency) {
   // one workgroup per bin (accumulation of the entries k_msm_sort ordered), then the bin
   // reductions (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
   if (acc_begin) (void)hipEventRecord(acc_begin, st);      // timed batches: the accumulation alone
@@ -1068,7 +1079,11 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
                        buckets, heads, slice_W, slice_T);
   if (acc_end) (void)hipEventRecord(acc_end, st);
   if ((probe_skip & 64) || EDC_FUSED_REDUCE) return;
-  if (P.nbin() <= REDUCE_QUAD_MAX_BINS)
+  // latency: one synchronous batch on an idle GPU (edc_batch_verify*): the quad-cooperative weighted
+  // sum (one workgroup per bin) has ~1/3 of the lane-parallel form's serial instruction count per
+  // wave -- a lone wave issues one VALU instruction per ~5.5 cycles whatever its dependencies --
+  // at ~2x its VALU work, which only the pipelined submissions (other batches to overlap) mind
+  if (P.nbin() <= REDUCE_QUAD_MAX_BINS || (latency && P.nbin() <= REDUCE_QUAD_LATENCY_MAX_BINS))
     hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
   else if (P.nbin() < REDUCE64_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
