@@ -185,7 +185,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="workload; c3 (configs[2]) is the one BASELINE.json's metric is quoted on")
-    ap.add_argument("--n", type=int, default=None, help="signatures per GPU per step (default: the config's)")
+    ap.add_argument("--n", "--batch", dest="n", type=int, default=None,
+                    help="signatures per GPU per step (default: the config's; --batch under torch.distributed.run, "
+                         "whose own parser takes --n for an abbreviation of its options)")
     ap.add_argument("--keys", type=int, default=None, help="validators (0 = distinct keys; default: the config's)")
     ap.add_argument("--msg-len", type=int, default=None, help="message bytes (-1 = uniform 0..1024)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
@@ -213,8 +215,10 @@ def main():
                          "Item {vk_bytes, sig, k}); SHA-512 is then outside the timed region (not the headline)")
     ap.add_argument("--scatter-stage", type=int, default=0,
                     help="measurement only: cap the binning scatter's LDS stage (entries; edc_debug_set_scatter_stage)")
-    ap.add_argument("--exchange-lag", type=int, default=4,
-                    help="multi-rank: partial-point exchanges (all-gathers) in flight before the oldest is combined")
+    ap.add_argument("--exchange-lag", type=int, default=8,
+                    help="multi-rank: batches whose exchange is in flight before the oldest verdict is completed")
+    ap.add_argument("--exchange-group", type=int, default=4,
+                    help="multi-rank: batches whose records leave in one all-gather (sharded.ExchangeRing)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args()
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
@@ -238,6 +242,9 @@ def main():
     force_dist = os.environ.get("EDC_FORCE_DIST") == "1"
     if world > 1 or force_dist:
         import torch.distributed as dist
+        # RCCL's streams at high priority: the per-group collective must not queue behind the
+        # in-flight batches' kernels for a free CU
+        os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     dev = torch.device(f"cuda:{local}")
@@ -256,12 +263,17 @@ def main():
     sharing = max(1, -(-world // max(1, torch.cuda.device_count()))) if backend == "gloo" else 1
     slots = max(1, 16 // sharing)
     nmb = max(1, args.multi)                       # batches per launch sequence
+    inflight_auto = args.inflight <= 0
+    # small shards want 16 batches in flight, one hardware queue each; a multi-rank run adds the
+    # exchange ring's stream and RCCL's own, and past ~16 user queues the scheduler time-slices
+    # them ("One hardware queue per in-flight slot"), so it keeps 12
+    small_depth = 12 if (world > 1 or force_dist) else 16
     if args.inflight <= 0:
         if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh;
             # union first measured 6.38e8 at 3 and 5.55e8 at 6 at 8 x 2^17, profiles/r04/r04w_union_inflight6_summary.log)
             args.inflight = 3 if n * nmb >= (1 << 19) else 4
         else:
-            args.inflight = 6 if n >= (1 << 19) else 16
+            args.inflight = 6 if n >= (1 << 19) else small_depth
     args.inflight = min(args.inflight, slots)
     if nmb > 1:    # every slot's multi-batch workspace is allocated on its first launch: warm them all
         args.warmup = max(args.warmup, args.inflight + 1)
@@ -297,7 +309,8 @@ def main():
     # device, gloo on the host for the one-GPU rehearsals); up to --exchange-lag are in flight
     # (RCCL: the gathered records are combined on the device right behind the collective)
     ring = (sharded.ExchangeRing(dist, dev if backend != "gloo" else torch.device("cpu"), depth=args.exchange_lag,
-                                 device_combine=eng if backend != "gloo" else None) if dist else None)
+                                 device_combine=eng if backend != "gloo" else None, group=args.exchange_group)
+            if dist else None)
     xstat = {"post": 0.0, "pop": 0.0, "combine": 0.0}
 
     def timed_ring_op(f, name):
@@ -402,19 +415,26 @@ def main():
         # multi-rank: the other scaling shape beside the headline one, on the same ranks and data
         # (strong: the ranks split one --n batch; weak: every rank verifies --n of its own), so a
         # SCALE record carries both; items are a prefix of this rank's slice, z at global indices
-        n_main, base_main = n, base
+        n_main, base_main, inflight_main = n, base, args.inflight
         n = args.n if args.scaling == "strong" else args.n // world
         base = rank * n
+        if inflight_auto:              # the in-flight depth the default picks for this shard size
+            args.inflight = min(6 if n >= (1 << 19) else small_depth, slots)
+            eng._check(lib.edc_set_slots(eng.ctx, args.inflight))
         eng._check(lib.edc_reserve(eng.ctx, n))
         if n <= n_main:
             run_steps(max(2, args.warmup))
             el2, codes2 = timed(args.steps)
             other = {"scaling": "weak" if args.scaling == "strong" else "strong", "sigs_per_gpu": n,
+                     "inflight": args.inflight,
                      "value": round(n * world * args.steps / el2, 1), "ms_per_step": round(el2 / args.steps * 1e3, 3),
                      "verdict_ok": all(c == 0 for c in codes2)}
         else:
             other = {"scaling": "weak", "skipped": "the weak shape needs --n per rank; this rank holds --n / world"}
         n, base = n_main, base_main
+        if args.inflight != inflight_main:
+            args.inflight = inflight_main
+            eng._check(lib.edc_set_slots(eng.ctx, args.inflight))
     verdict_ok = all(c == 0 for c in codes)
     # an A/B build (--lib, tools/ab_variants.sh) may be a timing probe that is wrong by design:
     # report its verdicts instead of stopping; the product library must verify the batch
@@ -523,7 +543,7 @@ def main():
                        "parallelism": f"shard{world}" if world > 1 else "single"},
             # the process group the ranks actually formed (None: one process, no collectives)
             "comm": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
-                      "exchange_lag": args.exchange_lag,
+                      "exchange_lag": args.exchange_lag, "exchange_group": args.exchange_group,
                       "exchange_us": exchange_us,
                       "exchange_note": "host time per batch inside the timed loop: posting the all-gather, "
                                        "completing it (waits for the collective), combining the partials"}

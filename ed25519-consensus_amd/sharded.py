@@ -79,88 +79,111 @@ def torch_allgather_fn(dist, device):
 
 class ExchangeRing:
     """Pipelined exchange of one fixed-size record per rank and batch (the 129-byte partial +
-    reject flag), with up to `depth` exchanges in flight: post() starts the all-gather of a batch
-    and returns at once, pop() completes the OLDEST one and returns its per-rank records (rank
-    order). Every rank posts its batches in the same order, so collective i matches batch i on all
-    ranks; the verdicts still complete in queue order.
+    reject flag). post() queues a batch's record and returns at once; every `group` records leave
+    in ONE all-gather (group x 129 bytes per rank), so the per-collective costs -- the host's
+    launch of the copies, the collective and the combine, and the collective's wait for a free CU
+    on a full device -- are paid once per group; pop() completes the OLDEST batch (sending a
+    partial group first if it is still pending) and returns its per-rank records (rank order).
+    Every rank runs the same post/pop sequence, so the collectives match on all ranks and the
+    verdicts complete in queue order.
 
-    On a GPU device (RCCL) the staging copies and the collective run on a private non-blocking
-    torch stream: the host never waits for the collective inside post(), and the engine's slot
-    streams (blocking streams, hipExtStreamCreateWithCUMask takes no flags) never wait behind it.
-    Each in-flight exchange owns its pinned host and device buffers, reused only after pop().
-    On the CPU (gloo) the collective is async_op=True and pop() waits for its work handle.
+    On a GPU device (RCCL) the staging copies, the collective and the combine run on a private
+    high-priority non-blocking torch stream: the host never waits for the collective inside
+    post(), and the engine's slot streams (blocking streams, hipExtStreamCreateWithCUMask takes no
+    flags) never wait behind it. Each group in flight owns its pinned host and device buffers,
+    reused only after its last pop(). On the CPU (gloo) the collective is async_op=True and pop()
+    waits for its work handle.
 
-    device_combine (GPU only): an Engine. The combine of the gathered records is then enqueued on
-    the same side stream right behind the collective (edc_combine_records_device: sum, x8,
-    identity test on the device, no host round trip of the records), and pop() returns the
+    device_combine (GPU only): an Engine. The combine of each batch's gathered records is then
+    enqueued on the same side stream right behind the collective (edc_combine_records_device: sum,
+    x8, identity test on the device, no host round trip of the records), and pop() returns the
     verdict code instead of the records (`combines` is True)."""
 
-    def __init__(self, dist, device, rec_len=129, depth=4, device_combine=None):
+    def __init__(self, dist, device, rec_len=129, depth=4, device_combine=None, group=1):
         import torch
-        self.dist, self.n = dist, rec_len
+        self.dist, self.n, self.K = dist, rec_len, max(1, group)
         self.world = dist.get_world_size()
         self.gpu = device.type != "cpu"
         self.eng = device_combine if self.gpu else None
         self.combines = self.eng is not None
-        self.q = []
-        nbuf = depth + 1
+        self.pending = []                 # records of the group being filled
+        self.sent = []                    # [buffer index, records in the group, handle, records popped]
+        nbuf = (depth + self.K) // self.K + 1
+        K, n, W = self.K, rec_len, self.world
         if self.gpu:
-            self.side = torch.cuda.Stream(device=device)
-            nres = 256 if self.combines else self.world * rec_len      # result block / the records
+            self.side = torch.cuda.Stream(device=device, priority=-1)
+            nres = 256 * K if self.combines else W * K * n      # result blocks / the records
             with torch.cuda.stream(self.side):
-                self.bufs = [(torch.empty(rec_len, dtype=torch.uint8, pin_memory=True),
+                self.bufs = [(torch.empty(K * n, dtype=torch.uint8, pin_memory=True),
                               torch.empty(nres, dtype=torch.uint8, pin_memory=True),
-                              torch.empty(rec_len, dtype=torch.uint8, device=device),
-                              torch.empty(self.world * rec_len, dtype=torch.uint8, device=device),
-                              torch.empty(256, dtype=torch.uint8, device=device))
+                              torch.empty(K * n, dtype=torch.uint8, device=device),
+                              torch.empty(W * K * n, dtype=torch.uint8, device=device),
+                              torch.empty(256 * K, dtype=torch.uint8, device=device))
                              for _ in range(nbuf)]
         else:
-            self.bufs = [(torch.empty(rec_len, dtype=torch.uint8), torch.empty(self.world * rec_len, dtype=torch.uint8))
+            self.bufs = [(torch.empty(K * n, dtype=torch.uint8), torch.empty(W * K * n, dtype=torch.uint8))
                          for _ in range(nbuf)]
         self.free = list(range(nbuf))
 
     def __len__(self):
-        return len(self.q)
+        return len(self.pending) + sum(cnt - done for _, cnt, _, done in self.sent)
 
     def post(self, rec):
+        assert len(rec) == self.n
+        self.pending.append(bytes(rec))
+        if len(self.pending) == self.K:
+            self._send()
+
+    def _send(self):
         import numpy as np
         import torch
-        assert len(rec) == self.n
         if not self.free:
             raise RuntimeError("ExchangeRing: more exchanges in flight than its depth; pop() first")
         i = self.free.pop()
+        cnt, K, n = len(self.pending), self.K, self.n
+        blob = b"".join(self.pending) + bytes((K - cnt) * n)      # a partial group is padded
+        self.pending = []
         if self.gpu:
             h_in, h_out, d_in, d_out, d_res = self.bufs[i]
             with torch.cuda.stream(self.side):
-                h_in.numpy()[:] = np.frombuffer(rec, dtype=np.uint8)
+                h_in.numpy()[:] = np.frombuffer(blob, dtype=np.uint8)
                 d_in.copy_(h_in, non_blocking=True)
                 work = self.dist.all_gather_into_tensor(d_out, d_in, async_op=True)
                 work.wait()              # the side stream waits for the collective; the host does not
-                if self.combines:
-                    self.eng.combine_records_device(self.side.cuda_stream, self.world, d_out.data_ptr(), self.n,
-                                                    d_res.data_ptr())
+                if self.combines:        # batch k of the group: rank r's record at r K n + k n
+                    for k in range(cnt):
+                        self.eng.combine_records_device(self.side.cuda_stream, self.world, d_out.data_ptr() + k * n,
+                                                        K * n, d_res.data_ptr() + 256 * k)
                     h_out.copy_(d_res, non_blocking=True)
                 else:
                     h_out.copy_(d_out, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.side)
-            self.q.append((i, ev))
+            self.sent.append([i, cnt, ev, 0])
         else:
             t_in, t_out = self.bufs[i]
-            t_in.numpy()[:] = np.frombuffer(rec, dtype=np.uint8)
-            self.q.append((i, self.dist.all_gather_into_tensor(t_out, t_in, async_op=True)))
+            t_in.numpy()[:] = np.frombuffer(blob, dtype=np.uint8)
+            self.sent.append([i, cnt, self.dist.all_gather_into_tensor(t_out, t_in, async_op=True), 0])
 
     def pop(self):
-        i, h = self.q.pop(0)
-        if self.gpu:
-            h.synchronize()
-        else:
-            h.wait()
-        host = self.bufs[i][1].numpy().tobytes()
-        self.free.append(i)
+        if not self.sent:
+            self._send()                 # the oldest batch is still in the group being filled
+        g = self.sent[0]
+        i, cnt, h, k = g
+        if k == 0:
+            if self.gpu:
+                h.synchronize()
+            else:
+                h.wait()
+        g[3] += 1
+        if g[3] == cnt:
+            self.sent.pop(0)
+            self.free.append(i)
+        host = self.bufs[i][1].numpy()
         if self.combines:                # the device's verdict word: 0 Ok, 1 reject
-            return int.from_bytes(host[:4], "little")
-        return [host[r * self.n:(r + 1) * self.n] for r in range(self.world)]
+            return int.from_bytes(host[256 * k:256 * k + 4].tobytes(), "little")
+        K, n = self.K, self.n
+        return [host[r * K * n + k * n:r * K * n + (k + 1) * n].tobytes() for r in range(self.world)]
 
 
 def run_sharded_stream(k, inflight, submit_fn, wait_fn, combine_fn, ring, lag):

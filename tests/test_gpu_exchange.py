@@ -68,9 +68,11 @@ def _free_port():
     return p
 
 
-def test_exchange_ring_rccl_single_rank(engine):
+@pytest.mark.parametrize("group", [1, 3])
+def test_exchange_ring_rccl_single_rank(engine, group):
     """ExchangeRing over a one-rank RCCL group with the device combine: several exchanges in
-    flight, completed in order, each giving its batch's fixture verdict."""
+    flight (one record or `group` records per all-gather), completed in order, each giving its
+    batch's fixture verdict."""
     torch = pytest.importorskip("torch")
     import torch.distributed as dist
     from conftest import load_pkg
@@ -81,7 +83,7 @@ def test_exchange_ring_rccl_single_rank(engine):
     dist.init_process_group("nccl", rank=0, world_size=1)
     try:
         dev = torch.device("cuda:0")
-        ring = sharded.ExchangeRing(dist, dev, depth=3, device_combine=engine)
+        ring = sharded.ExchangeRing(dist, dev, depth=3, device_combine=engine, group=group)
         assert ring.combines
         stream = [BATCHES[i % len(BATCHES)] for i in range(2 * len(BATCHES))]
         recs = {id(b): _partials(engine, torch, b, 1)[0] for b in BATCHES}

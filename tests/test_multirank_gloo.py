@@ -73,7 +73,7 @@ STREAM = ["mixed_corpus_one_bad", "repeated_keys_varlen", "undecodable_R", "batc
           "repeated_keys_varlen", "mixed_corpus_one_bad"]
 
 
-def _stream_worker(rank, world, port, inflight, lag, out_path):
+def _stream_worker(rank, world, port, inflight, lag, group, out_path):
     """bench.py's multi-rank loop (sharded.run_sharded_stream + ExchangeRing over gloo): a stream of
     golden batches, `inflight` submitted ahead, `lag` all-gathers in flight; the oracle computes
     each rank's partial where the GPU runs edc_batch_wait(partial)."""
@@ -109,20 +109,23 @@ def _stream_worker(rank, world, port, inflight, lag, out_path):
         code, _ = oracle_c.combine_affine([p[:64] for p in parts])
         return 1 if bad_any else code
 
-    ring = sharded.ExchangeRing(dist, torch.device("cpu"), depth=lag)
+    ring = sharded.ExchangeRing(dist, torch.device("cpu"), depth=lag, group=group)
     codes = sharded.run_sharded_stream(len(STREAM), inflight, submit, wait, combine, ring, lag)
     with open(out_path + f".{rank}", "w") as f:
         json.dump({"codes": codes, "log": log}, f)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,inflight,lag", [(2, 1, 1), (4, 3, 2), (8, 4, 3)])
-def test_stream_loop_in_order(tmp_path, world, inflight, lag):
+@pytest.mark.parametrize("world,inflight,lag,group", [(2, 1, 1, 1), (4, 3, 2, 1), (8, 4, 3, 1), (4, 3, 5, 2),
+                                                     (8, 4, 8, 3)])
+def test_stream_loop_in_order(tmp_path, world, inflight, lag, group):
     """The multi-rank loop of bench.py at 2 / 4 / 8 ranks with several batches and exchanges in
-    flight: every rank gets every batch's unsharded verdict, in batch order; a batch is submitted
-    up to `inflight` ahead of its collection (the refill precedes the exchange)."""
+    flight, one record or a group of records per all-gather (partial groups flushed when the
+    oldest verdict is needed): every rank gets every batch's unsharded verdict, in batch order; a
+    batch is submitted up to `inflight` ahead of its collection (the refill precedes the
+    exchange)."""
     out = str(tmp_path / "stream")
-    mp.start_processes(_stream_worker, args=(world, _free_port(), inflight, lag, out), nprocs=world, join=True,
+    mp.start_processes(_stream_worker, args=(world, _free_port(), inflight, lag, group, out), nprocs=world, join=True,
                        start_method="spawn")
     gold = {x["name"]: x for x in golden("batches.json")["batches"]}
     expect = [gold[nm]["expect_code"] for nm in STREAM]
