@@ -110,7 +110,8 @@ def load_library(path=None):
         lib.edc_batch_partial_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                  c_vp, ctypes.POINTER(ctypes.c_int)]
         lib.edc_combine_partials.argtypes = [c_vp, c_sz, c_u8p, ctypes.c_int, c_vp]
-        lib.edc_combine_records_device.argtypes = [c_vp, c_vp, c_sz, c_vp, c_sz, c_vp]
+        if hasattr(lib, "edc_combine_records_device"):      # absent from older A/B builds (--lib)
+            lib.edc_combine_records_device.argtypes = [c_vp, c_vp, c_sz, c_vp, c_sz, c_vp]
         lib.edc_batch_submit_device.restype = ctypes.c_int64
         lib.edc_batch_submit_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                 ctypes.c_int]

@@ -11,6 +11,8 @@
 #   driver           the driver's bench command (--gpus 1 --steps 20 --warmup 5, with the CPU baseline)
 #   c3 | c2 | c5     40-step benches of configs[2] / configs[1] / configs[4] (no CPU baseline)
 #   n17 | n18 | n19  2^17 / 2^18 / 2^19 shards of the vote batch (strong-scaling per-GPU rates)
+#   n17s | c2s       2^17 shards / configs[1] over 1600 steps: the steady state (40 steps of a
+#                    0.25 ms batch are mostly the fill and drain of 16 batches in flight)
 #   fallback         tools/fallback_bench.py (configs[3])    host  tools/host_bench.py
 #   small            tools/smallbatch_bench.py               multi tools/multi_bench.py
 #   prof             rocprofv3 kernel-trace stats of the bench, one batch at a time and pipelined
@@ -67,6 +69,8 @@ for step in "$@"; do
     c2) bench_step c2 --config c2 --steps 40 --warmup 5 --no-cpu-baseline ;;
     c5) bench_step c5 --config c5 --steps 12 --warmup 3 --no-cpu-baseline ;;
     n17) bench_step n17 --n 131072 --steps 40 --warmup 5 --no-cpu-baseline ;;
+    n17s) bench_step n17s --n 131072 --steps 1600 --warmup 5 --no-cpu-baseline ;;
+    c2s) bench_step c2s --config c2 --steps 1600 --warmup 5 --no-cpu-baseline ;;
     n18) bench_step n18 --n 262144 --steps 40 --warmup 5 --no-cpu-baseline ;;
     n19) bench_step n19 --n 524288 --steps 40 --warmup 5 --no-cpu-baseline ;;
     bench=*) a=${step#bench=}; bench_step bench ${a//,/ } ;;
