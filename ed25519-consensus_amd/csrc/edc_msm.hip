@@ -423,13 +423,6 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
 #ifndef EDC_ACC_OCC
 #define EDC_ACC_OCC 4
 #endif
-// 1: the accumulation workgroup reduces its own bin after the heads merge (weighted_sum_256 over
-// the 256 bucket sums, in the LDS the row buffers used), so no separate reduction kernel runs
-#ifndef EDC_FUSED_REDUCE
-#define EDC_FUSED_REDUCE 0
-#endif
-constexpr int ACC_LDS_WORDS = EDC_FUSED_REDUCE && NSLICE * EXT_WORDS > 4 * WAVE_ROWS_WORDS ? NSLICE * EXT_WORDS
-                                                                                             : 4 * WAVE_ROWS_WORDS;
 #ifndef EDC_ACC_HOIST
 #define EDC_ACC_HOIST 0   // measurement knob: let the compiler hoist the DMA piece map (needs VGPRs)
 #endif
@@ -449,7 +442,7 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
 #ifndef EDC_ACC_LDS_PAD
 #define EDC_ACC_LDS_PAD 0   // measurement knob: extra LDS words per workgroup (caps workgroups per CU)
 #endif
-  __shared__ __attribute__((aligned(16))) uint32_t lbuf[ACC_LDS_WORDS + EDC_ACC_LDS_PAD];   // row buffers of the 4 waves
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[4 * WAVE_ROWS_WORDS + EDC_ACC_LDS_PAD];   // row buffers of the 4 waves
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
   const uint32_t bin = blockIdx.x;
@@ -554,24 +547,6 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
     st_ext(bucket_slot(buckets, bin, cb), acc);
   }
   ACC_STAMP(3, __builtin_amdgcn_s_memtime());
-#if EDC_FUSED_REDUCE
-  // the bin's reduction, W = sum_t (t+1) S_t and T = sum_t S_t (k_msm_reduce_quad's weighted sum):
-  // every bucket sum is final in `buckets` after the barrier (the same workgroup wrote them, as the
-  // heads above); staged into the LDS the row buffers used
-  __threadfence_block();
-  __syncthreads();
-  st_ext(lbuf + t * EXT_WORDS, ld_ext(bucket_slot(buckets, bin, t)));
-  __syncthreads();
-  ge_p3 ws, tot;
-  weighted_sum_256(lbuf, lbuf, lbuf + 64 * EXT_WORDS, ws, tot);
-  if (t < 4) {
-    const ge_p3 W = quad_add(ws, tot);              // sum_t (t + 1) S_t
-    if (t == 0) {
-      st_ext(slice_W + (size_t)bin * EXT_WORDS, W);
-      st_ext(slice_T + (size_t)bin * EXT_WORDS, tot);
-    }
-  }
-#endif
   ACC_STAMP(6, __builtin_amdgcn_s_memrealtime());
 }
 
@@ -655,10 +630,14 @@ constexpr uint32_t REDUCE_QUAD_LATENCY_MAX_BINS = EDC_REDUCE_QUAD_LATENCY_MAX_BI
 #define EDC_REDUCE64_MAX_BINS 256
 #endif
 constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per bin below this many bins
+// lanes per bin from that many bins up: pipelined batches take 16 (the least VALU work: 672 point
+// additions per bin against 864 with 32; the chip runs at its power limit, so instructions, not
+// serial depth, set the pipeline's rate), synchronous calls 32 (half the serial depth)
 #ifndef EDC_REDUCE_WIDE_LANES
-#define EDC_REDUCE_WIDE_LANES 32
+#define EDC_REDUCE_WIDE_LANES 16
 #endif
-constexpr int REDUCE_WIDE_LANES = EDC_REDUCE_WIDE_LANES;          // lanes per bin from that many bins up
+constexpr int REDUCE_WIDE_LANES = EDC_REDUCE_WIDE_LANES;
+constexpr int REDUCE_LATENCY_LANES = 32;
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ buckets,
                                                          uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
@@ -1078,7 +1057,7 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
     hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
                        buckets, heads, slice_W, slice_T);
   if (acc_end) (void)hipEventRecord(acc_end, st);
-  if ((probe_skip & 64) || EDC_FUSED_REDUCE) return;
+  if (probe_skip & 64) return;
   // latency: one synchronous batch on an idle GPU (edc_batch_verify*): the quad-cooperative weighted
   // sum (one workgroup per bin) has ~1/3 of the lane-parallel form's serial instruction count per
   // wave -- a lone wave issues one VALU instruction per ~5.5 cycles whatever its dependencies --
@@ -1088,6 +1067,9 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
   else if (P.nbin() < REDUCE64_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
                        slice_T);
+  else if (latency)
+    hipLaunchKernelGGL(k_msm_reduce<REDUCE_LATENCY_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_LATENCY_LANES)), dim3(256),
+                       0, st, P.nbin(), counts, buckets, slice_W, slice_T);
   else
     hipLaunchKernelGGL(k_msm_reduce<REDUCE_WIDE_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_WIDE_LANES)), dim3(256), 0, st,
                        P.nbin(), counts, buckets, slice_W, slice_T);
