@@ -175,6 +175,15 @@ def test_sha512_challenge_scalars_chacha(hc, oracle):
         for op, exp in [(0, a * c), (1, a + c), (2, a - c), (3, (a % (1 << 128)) * c)]:
             hc.hc_sc_op(op, b32(a), b32(c), out)
             assert int.from_bytes(out.raw[:32], "little") == exp % L
+    # the folds' boundaries: multiples of l and their neighbours, 2^252 / 2^260 / 2^385 edges,
+    # all-ones, single bits (each fold's sign and carry cases)
+    edges = [0, 1, L - 1, L, L + 1, 2 * L - 1, 2 * L, 2**252 - 1, 2**252, 2**253, 2**260 - 1,
+             2**385, 2**512 - 1, 2**511, ((2**512 - 1) // L) * L, ((2**512 - 1) // L) * L - 1]
+    edges += [1 << b for b in range(0, 512, 7)] + [(1 << b) - 1 for b in range(1, 513, 13)]
+    edges += [k * L + d for k in [1, 3, 2**130, 2**259] for d in [-1, 0, 1]]
+    for x in edges:
+        hc.hc_sc_reduce_wide(x.to_bytes(64, "little"), out)
+        assert int.from_bytes(out.raw[:32], "little") == x % L, hex(x)
     for v in [0, L - 1, L, L + 1, 2**255, 2**256 - 1]:
         assert hc.hc_sc_is_canonical(b32(v)) == (v < L)
     for key in [bytes(32), bytes([0x33]) * 32]:
