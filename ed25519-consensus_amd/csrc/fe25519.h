@@ -270,11 +270,33 @@ EDC_HD void fe_to_words(const fe& a, uint32_t w[8]) {
 
 EDC_HD bool fe_is_negative(const fe& a) { return fe_canon(a).v[0] & 1u; }
 
+// a == 0 (mod p) without the full canonical form: one serial carry, one fold of the bits >= 255
+// (2^255 == 19) and a second carry give a value V < 2^255 + 2^13 < 2p in 29-bit limbs, so
+// a == 0 iff V is 0 or p.
 EDC_HD bool fe_is_zero(const fe& a) {
-  fe c = fe_canon(a);
-  uint32_t o = 0;
-  for (int i = 0; i < 9; ++i) o |= c.v[i];
-  return o == 0;
+  uint32_t r[9], c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t t = a.v[i] + c;                 // a.v[i] < 2^30.41, c < 2^4
+    r[i] = t & M29;
+    c = t >> 29;
+  }
+  uint32_t t8 = a.v[8] + c;
+  c = (t8 >> 23) * 19u;
+  r[8] = t8 & 0x7FFFFFu;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t t = r[i] + c;
+    r[i] = t & M29;
+    c = t >> 29;
+  }
+  r[8] += c;
+  uint32_t z = 0, q = (r[0] ^ (M29 - 18u)) | (r[8] ^ 0x7FFFFFu);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) z |= r[i];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) q |= r[i] ^ M29;
+  return z == 0 || q == 0;
 }
 
 EDC_HD bool fe_eq(const fe& a, const fe& b) {

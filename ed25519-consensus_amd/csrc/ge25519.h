@@ -24,7 +24,10 @@ EDC_HD ge_niels ge_niels_identity() {
   ge_niels r; r.ypx = fe_one(); r.ymx = fe_one(); r.xy2d = fe_zero(); return r;
 }
 
-// dalek FieldElement::sqrt_ratio_i. Returns was_nonzero_square; r = nonnegative root.
+// dalek FieldElement::sqrt_ratio_i as decoding uses it. Returns was_nonzero_square (or u == 0);
+// when it holds, r is a root of u/v of either sign (ge_decompress fixes the sign in the same
+// select that applies the encoding's sign bit). dalek's third test (check == -u sqrt(-1)) only
+// changes r when the result is rejected, so it is not computed.
 EDC_HD bool fe_sqrt_ratio_i(const fe& u, const fe& v, fe& r) {
   fe v3 = fe_mul(fe_sqr(v), v);
   fe v7 = fe_mul(fe_sqr(v3), v);
@@ -33,14 +36,11 @@ EDC_HD bool fe_sqrt_ratio_i(const fe& u, const fe& v, fe& r) {
   // a == b (mod p) tested as canon(a - b) == 0: one canonicalisation per test instead of two
   bool correct = fe_is_zero(fe_sub(check, u));                        // check == u
   bool flipped = fe_is_zero(fe_add(check, u));                        // check == -u
-  bool flipped_i = fe_is_zero(fe_add(check, fe_mul(u, fe_sqrtm1())));  // check == -u * sqrt(-1)
-  fe r_prime = fe_mul(fe_sqrtm1(), r);
-  r = fe_select(r, r_prime, flipped || flipped_i);
-  r = fe_select(r, fe_neg(r), fe_is_negative(r));
+  r = fe_select(r, fe_mul(fe_sqrtm1(), r), flipped);
   return correct || flipped;
 }
 
-// ZIP215 decode: y = bytes & (2^255-1) (NOT reduced), x from sqrt_ratio_i, negate iff bit 255.
+// ZIP215 decode: y = bytes & (2^255-1) (NOT reduced), x from sqrt_ratio_i, negative iff bit 255.
 // Returns false iff the y coordinate is not on the curve.
 EDC_HD bool ge_decompress(const uint32_t w[8], ge_p3& P) {
   fe Y = fe_from_words(w);
@@ -50,8 +50,8 @@ EDC_HD bool ge_decompress(const uint32_t w[8], ge_p3& P) {
   fe v = fe_add_c(fe_mul(YY, fe_d()), one);
   fe X;
   bool ok = fe_sqrt_ratio_i(u, v, X);
-  bool sign = (w[7] >> 31) != 0;
-  X = fe_select(X, fe_neg(X), sign);
+  const bool sign = (w[7] >> 31) != 0;
+  X = fe_select(X, fe_neg(X), fe_is_negative(X) != sign);   // |x|, then negated iff the sign bit
   P.X = X;
   P.Y = fe_carry(Y);
   P.Z = one;

@@ -57,6 +57,13 @@ void hc_fe_limbs(int op, const uint32_t* a, const uint32_t* b, uint8_t* out, uin
   words_to_bytes(wo, out);
 }
 
+// fe_is_zero on raw limbs (any form with limbs < 2^30.41)
+int hc_fe_is_zero_limbs(const uint32_t* a) {
+  fe x;
+  for (int i = 0; i < 9; ++i) x.v[i] = a[i];
+  return fe_is_zero(x) ? 1 : 0;
+}
+
 // stress the lazy bounds: r = ((a+b)*(c+d) - (a*b)) chained k times
 void hc_fe_chain(const uint8_t* a, const uint8_t* b, int k, uint8_t* out) {
   uint32_t wa[8], wb[8], wo[8];

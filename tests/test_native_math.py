@@ -190,3 +190,46 @@ def test_sha512_challenge_scalars_chacha(hc, oracle):
         for ctr in [0, 1, 7, 2**32 + 1]:
             hc.hc_chacha_block(key, ctypes.c_uint64(ctr), out)
             assert out.raw == oracle.chacha20_block(key, ctr)
+
+
+def test_fe_is_zero_lazy_limbs(hc):
+    """fe_is_zero's short form (one fold, compare with 0 and p) on every multiple of p that the
+    lazy limb bound (< 2^30.41 per limb) can hold, in normalized and carry-shifted limb forms, and
+    on random non-zero neighbours."""
+    P = 2**255 - 19
+    bound = int(2**30.41)
+    rnd = random.Random(11)
+
+    def limbs(v):
+        return [(v >> (29 * i)) & ((1 << 29) - 1) if i < 8 else v >> 232 for i in range(9)]
+
+    def call(ls):
+        assert all(0 <= x < bound for x in ls)
+        return hc.hc_fe_is_zero_limbs((ctypes.c_uint32 * 9)(*ls))
+
+    checked = 0
+    for k in range(0, 2**262 // P):
+        base = limbs(k * P)
+        if base[8] >= bound:
+            break
+        forms = [base]
+        for _ in range(6):                    # move 2^29 down from limb i+1 into limb i
+            f = list(forms[-1])
+            i = rnd.randrange(8)
+            if f[i + 1] > 0 and f[i] + (1 << 29) < bound:
+                f[i + 1] -= 1
+                f[i] += 1 << 29
+            forms.append(f)
+        for f in forms:
+            assert call(f) == 1, (k, f)
+            g = list(f)
+            g[rnd.randrange(9)] ^= 1 << rnd.randrange(20)
+            v = sum(x << (29 * i) for i, x in enumerate(g))
+            if all(x < bound for x in g):
+                assert call(g) == (1 if v % P == 0 else 0)
+            checked += 1
+    assert checked > 50
+    for _ in range(2000):
+        ls = [rnd.randrange(bound) for _ in range(9)]
+        v = sum(x << (29 * i) for i, x in enumerate(ls))
+        assert call(ls) == (1 if v % P == 0 else 0)
