@@ -630,14 +630,14 @@ constexpr uint32_t REDUCE_QUAD_LATENCY_MAX_BINS = EDC_REDUCE_QUAD_LATENCY_MAX_BI
 #define EDC_REDUCE64_MAX_BINS 256
 #endif
 constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per bin below this many bins
-// lanes per bin from that many bins up: pipelined batches take 16 (the least VALU work: 672 point
-// additions per bin against 864 with 32; the chip runs at its power limit, so instructions, not
-// serial depth, set the pipeline's rate), synchronous calls 32 (half the serial depth)
+// lanes per bin from that many bins up. 16 lanes do the least VALU work (672 point additions per
+// bin against 864 with 32) but double the serial depth: one configs[2] batch's reduction 102 ->
+// 139 us (rocprof, one batch at a time) for a pipelined rate within noise (+0.3 %,
+// profiles/r05/r05y_reduce16_vs_32_ab.log), so 32
 #ifndef EDC_REDUCE_WIDE_LANES
-#define EDC_REDUCE_WIDE_LANES 16
+#define EDC_REDUCE_WIDE_LANES 32
 #endif
 constexpr int REDUCE_WIDE_LANES = EDC_REDUCE_WIDE_LANES;
-constexpr int REDUCE_LATENCY_LANES = 32;
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ buckets,
                                                          uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
@@ -1067,9 +1067,6 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
   else if (P.nbin() < REDUCE64_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
                        slice_T);
-  else if (latency)
-    hipLaunchKernelGGL(k_msm_reduce<REDUCE_LATENCY_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_LATENCY_LANES)), dim3(256),
-                       0, st, P.nbin(), counts, buckets, slice_W, slice_T);
   else
     hipLaunchKernelGGL(k_msm_reduce<REDUCE_WIDE_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_WIDE_LANES)), dim3(256), 0, st,
                        P.nbin(), counts, buckets, slice_W, slice_T);

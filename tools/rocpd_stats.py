@@ -1,27 +1,25 @@
-"""Per-kernel duration summary (like rocprofv3 --stats) from a rocprofv3 rocpd SQLite database.
-Usage: python tools/rocpd_stats.py gpurun_out/prof/run_results.db [out.csv]"""
-import csv
+"""Kernel statistics (rocprofv3 --stats layout: Name,Calls,TotalDurationNs,AverageNs,Percentage,
+MinNs,MaxNs) from a rocprofv3 kernel-trace database (<dir>/<name>_results.db, the default output
+format of this image's rocprofv3), for profiles/.
+
+  python tools/rocpd_stats.py gpurun_out/<tag>_prof1/k_results.db > profiles/.../kernel_stats.csv
+"""
 import sqlite3
 import sys
 
 
-def main():
-    db = sys.argv[1]
-    c = sqlite3.connect(db)
+def main(path):
+    c = sqlite3.connect(path)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
-    name_col = "name" if "name" in cols else "kernel_name"
-    rows = c.execute(f"select {name_col}, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) "
-                     f"from kernels group by {name_col} order by sum(end-start) desc").fetchall()
-    tot = sum(r[2] for r in rows) or 1
-    out = [["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"]]
-    for n, k, s, a, lo, hi in rows:
-        out.append([n.split("(")[0], k, s, round(a, 1), round(100.0 * s / tot, 2), lo, hi])
-    if len(sys.argv) > 2:
-        with open(sys.argv[2], "w", newline="") as f:
-            csv.writer(f).writerows(out)
-    for r in out:
-        print(",".join(str(x) for x in r))
+    name = "name" if "name" in cols else "kernel_name"
+    rows = c.execute(f"select {name}, count(*), sum(end - start), avg(end - start), min(end - start), "
+                     f"max(end - start) from kernels group by {name} order by sum(end - start) desc").fetchall()
+    total = sum(r[2] for r in rows) or 1
+    print("Name,Calls,TotalDurationNs,AverageNs,Percentage,MinNs,MaxNs")
+    for n, calls, tot, avg, mn, mx in rows:
+        short = n.split("(")[0].replace("void ", "")
+        print(f"{short},{calls},{tot},{avg:.1f},{100.0 * tot / total:.2f},{mn},{mx}")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1])
