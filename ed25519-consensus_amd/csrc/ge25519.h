@@ -29,9 +29,10 @@ EDC_HD ge_niels ge_niels_identity() {
 // select that applies the encoding's sign bit). dalek's third test (check == -u sqrt(-1)) only
 // changes r when the result is rejected, so it is not computed.
 EDC_HD bool fe_sqrt_ratio_i(const fe& u, const fe& v, fe& r) {
-  fe v3 = fe_mul(fe_sqr(v), v);
-  fe v7 = fe_mul(fe_sqr(v3), v);
-  r = fe_mul(fe_mul(u, v3), fe_pow_p58(fe_mul(u, v7)));
+  const fe v2 = fe_sqr(v);
+  const fe uv3 = fe_mul(u, fe_mul(v2, v));
+  const fe uv7 = fe_mul(uv3, fe_sqr(v2));             // u v^3 * v^4: one multiplication fewer than u * v^7
+  r = fe_mul(uv3, fe_pow_p58(uv7));
   fe check = fe_mul(v, fe_sqr(r));
   // a == b (mod p) tested as canon(a - b) == 0: one canonicalisation per test instead of two
   bool correct = fe_is_zero(fe_sub(check, u));                        // check == u
