@@ -167,6 +167,8 @@ class ExchangeRing:
 
     def pop(self):
         if not self.sent:
+            if not self.pending:
+                raise RuntimeError("ExchangeRing.pop: nothing posted")
             self._send()                 # the oldest batch is still in the group being filled
         g = self.sent[0]
         i, cnt, h, k = g
