@@ -505,8 +505,9 @@ class Engine:
     def combine_records_device(self, stream, g, d_records, stride, d_out):
         """Enqueue the combine of g gathered 129-byte exchange records (device memory) on `stream`
         (a raw HIP stream handle); the 256-byte result block lands in d_out (device)."""
-        self._check(self.lib.edc_combine_records_device(self.ctx, ctypes.c_void_p(stream), g, ctypes.c_void_p(d_records),
-                                                        stride, ctypes.c_void_p(d_out)))
+        with self._lock:
+            self._check(self.lib.edc_combine_records_device(self.ctx, ctypes.c_void_p(stream), g,
+                                                            ctypes.c_void_p(d_records), stride, ctypes.c_void_p(d_out)))
 
     def combine_partials(self, partials, bad_any, want_check8=True):
         check8 = ctypes.create_string_buffer(32) if want_check8 else None
