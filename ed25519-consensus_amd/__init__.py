@@ -51,7 +51,7 @@ ABI_SYMBOLS = [
     "edc_batch_verify_prehashed", "edc_batch_verify_prehashed_device", "edc_batch_submit_prehashed",
     "edc_batch_submit_prehashed_device", "edc_batch_verify_prehashed_fallback",
     "edc_batch_verify_prehashed_fallback_device", "edc_multi_route", "edc_multi_debug_force_staged",
-    "edc_batch_submit_multi_device", "edc_batch_wait_multi", "edc_combine_records_device",
+    "edc_batch_submit_multi_device", "edc_batch_wait_multi", "edc_combine_records_device", "edc_debug_sc_reduce_wide",
 ]
 
 
@@ -112,6 +112,8 @@ def load_library(path=None):
         lib.edc_combine_partials.argtypes = [c_vp, c_sz, c_u8p, ctypes.c_int, c_vp]
         if hasattr(lib, "edc_combine_records_device"):      # absent from older A/B builds (--lib)
             lib.edc_combine_records_device.argtypes = [c_vp, c_vp, c_sz, c_vp, c_sz, c_vp]
+        if hasattr(lib, "edc_debug_sc_reduce_wide"):
+            lib.edc_debug_sc_reduce_wide.argtypes = [c_vp, c_sz, c_vp, c_vp]
         lib.edc_batch_submit_device.restype = ctypes.c_int64
         lib.edc_batch_submit_device.argtypes = [c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, c_u8p, ctypes.c_uint64, c_vp,
                                                 ctypes.c_int]

@@ -1296,6 +1296,20 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
   return combine_points(ctx, g, partials, bad_any, check8, nullptr);
 }
 
+int edc_debug_sc_reduce_wide(edc_ctx* ctx, size_t n, const uint8_t* d_in, uint8_t* d_out) {
+  if (!ctx || (n && (!d_in || !d_out)) || n > (1u << 24)) return EDC_ERR_ARG;
+  if (n && (!aligned16(d_in) || !aligned16(d_out))) {
+    ctx->err = "device buffers must be 16-byte aligned";
+    return EDC_ERR_ARG;
+  }
+  CK(hipSetDevice(ctx->device));
+  Slot& s = ctx->slot[0];
+  launch_sc_reduce_wide(s.st, (uint32_t)n, reinterpret_cast<const uint32_t*>(d_in), reinterpret_cast<uint32_t*>(d_out));
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(s.st));
+  return 0;
+}
+
 int edc_combine_records_device(edc_ctx* ctx, void* stream, size_t g, const uint8_t* d_records, size_t stride,
                                uint8_t* d_out) {
   if (!ctx || !d_out || (g && !d_records) || stride < 129 || g > 4096) return EDC_ERR_ARG;

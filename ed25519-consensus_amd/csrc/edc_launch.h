@@ -39,6 +39,7 @@ void launch_range_prebad(hipStream_t st, uint32_t n, uint32_t rsize, const uint8
                          const uint8_t* keybad,
                          const uint32_t* key_index, bool per_sig, uint8_t* rbad, const int* flags = nullptr);
 void launch_init_basepoint(hipStream_t st, uint32_t* pts);
+void launch_sc_reduce_wide(hipStream_t st, uint32_t n, const uint32_t* in, uint32_t* out);
 void launch_gather_items(hipStream_t st, uint32_t c, const uint32_t* idx, const uint8_t* vk, const uint8_t* sig,
                          const uint32_t* k, uint8_t* out_vk, uint8_t* out_sig, uint32_t* out_k);
 // vk_out[i] = keys[reg[key_idx[i]]] (32 bytes each; key-indexed host submissions)

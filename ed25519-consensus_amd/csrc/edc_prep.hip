@@ -896,4 +896,21 @@ void launch_init_basepoint(hipStream_t st, uint32_t* pts) {
   hipLaunchKernelGGL(k_init_basepoint, dim3(1), dim3(64), 0, st, pts);
 }
 
+// test hook: n 64-byte LE integers -> n 32-byte canonical residues mod l (sc_reduce_wide, the
+// reduction of Scalar::from_hash), so the device build of the folds meets chosen edge values
+__global__ void __launch_bounds__(256) k_sc_reduce_wide(uint32_t n, const uint32_t* __restrict__ in,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = in[(size_t)i * 16 + j];
+  const sc r = sc_reduce_wide(x);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[(size_t)i * 8 + j] = r.v[j];
+}
+void launch_sc_reduce_wide(hipStream_t st, uint32_t n, const uint32_t* in, uint32_t* out) {
+  if (n) hipLaunchKernelGGL(k_sc_reduce_wide, dim3(cdiv(n, 256)), dim3(256), 0, st, n, in, out);
+}
+
 }  // namespace edc

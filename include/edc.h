@@ -394,6 +394,14 @@ int edc_set_msm_bin_entries(edc_ctx* ctx, int entries);
 int edc_debug_set_scatter_stage(uint32_t max_entries);
 
 /*
+ * Test hook: the device's wide scalar reduction (Scalar::from_hash after SHA-512, reference
+ * src/batch.rs:86-91) on n caller-chosen 64-byte little-endian integers d_in (device, 16-byte
+ * aligned) -> n canonical 32-byte residues mod l in d_out (device, 16-byte aligned), synchronous.
+ * Lets tests drive the reduction's fold boundaries, which SHA-512 outputs practically never hit.
+ */
+int edc_debug_sc_reduce_wide(edc_ctx* ctx, size_t n, const uint8_t* d_in, uint8_t* d_out);
+
+/*
  * Shape of the grouped fallback's range MSM (tuning / measurement): about `ranges` contiguous
  * ranges (1..1024, default 32) with `bits`-bit windows (8..13, default 10). The range count is
  * capped so that ranges x bins per range stays within the MSM's 8192 bins (e.g. at most 24 ranges

@@ -181,6 +181,7 @@ def test_sha512_challenge_scalars_chacha(hc, oracle):
              2**385, 2**512 - 1, 2**511, ((2**512 - 1) // L) * L, ((2**512 - 1) // L) * L - 1]
     edges += [1 << b for b in range(0, 512, 7)] + [(1 << b) - 1 for b in range(1, 513, 13)]
     edges += [k * L + d for k in [1, 3, 2**130, 2**259] for d in [-1, 0, 1]]
+    edges += [(h << 252) + rnd.getrandbits(rnd.randrange(1, 200)) for h in range(1, 300)]   # third fold < 0
     for x in edges:
         hc.hc_sc_reduce_wide(x.to_bytes(64, "little"), out)
         assert int.from_bytes(out.raw[:32], "little") == x % L, hex(x)
