@@ -1024,7 +1024,16 @@ void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_
       SB.grid_a = sgrid = cdiv(max_terms ? max_terms : 1, fa);
     }
   }
-  hipLaunchKernelGGL(k_msm_count, dim3(grid), dim3(256), nbin * sizeof(uint32_t), st, P, T, per, counts, flags);
+#ifndef EDC_COUNT_SPLIT
+#define EDC_COUNT_SPLIT 4
+#endif
+  // the count pass needs no long runs: EDC_COUNT_SPLIT times the scatter's workgroups (at 2^20, 257
+  // workgroups of 4096 terms leave one workgroup per CU, latency-bound: 49.5 us; 1,025 of 1024
+  // terms 34.0 us; past ~2,000 the per-workgroup flush of the bin counts to global atomics costs
+  // more, 84 us at 4,097; profiles/r05/r05ar, r05as)
+  const uint32_t cper = std::max(256u, per / EDC_COUNT_SPLIT);
+  hipLaunchKernelGGL(k_msm_count, dim3(cdiv(max_terms ? max_terms : 1, cper)), dim3(256), nbin * sizeof(uint32_t), st, P, T,
+                     cper, counts, flags);
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, st, nbin, counts, offsets, cursor);
 #ifdef EDC_PROBE_EXTRA_SCANS   // measurement only: N more (idempotent) dependent launches per batch
   for (int r = 0; r < EDC_PROBE_EXTRA_SCANS; ++r)
