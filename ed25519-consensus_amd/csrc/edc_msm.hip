@@ -369,6 +369,10 @@ __device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin
 // bucket, and empty buckets get the identity. A kernel of its own, so the memory-bound sort of one
 // batch overlaps the VALU-bound accumulation of another instead of idling the accumulation's CUs
 // (every workgroup of a launch sorts at the same time).
+#ifndef EDC_SORT_REG
+#define EDC_SORT_REG 40
+#endif
+constexpr int SORT_REG = EDC_SORT_REG;               // entries per lane held in registers (0: two reads)
 __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ counts,
                                                   const uint32_t* __restrict__ offsets,
                                                   const uint2* __restrict__ entries, uint32_t* __restrict__ sorted,
@@ -382,9 +386,17 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
   const uint32_t off = offsets[bin];
   lcnt[t] = 0;
   __syncthreads();
-  // loads are batched 8 deep so the passes are not latency-bound
+  // the first SORT_REG * 256 entries are read once and kept in registers for the second pass
+  // (a 2^20 batch's bins hold ~8k entries); any beyond are read twice, in batches of 8
+  uint2 reg[SORT_REG];
+#pragma unroll
+  for (int u = 0; u < SORT_REG; ++u)
+    reg[u] = t + 256u * u < E ? entries[off + t + 256u * u] : make_uint2(0u, 0xFFFFFFFFu);
+#pragma unroll
+  for (int u = 0; u < SORT_REG; ++u)
+    if (reg[u].y != 0xFFFFFFFFu) atomicAdd(&lcnt[reg[u].y], 1u);
   constexpr int SB = 8;
-  for (uint32_t e0 = t; e0 < E; e0 += 256 * SB) {
+  for (uint32_t e0 = t + 256u * SORT_REG; e0 < E; e0 += 256 * SB) {
     uint32_t y[SB];
 #pragma unroll
     for (int u = 0; u < SB; ++u) y[u] = e0 + 256u * u < E ? entries[off + e0 + 256u * u].y : 0xFFFFFFFFu;
@@ -410,7 +422,10 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
   }
   __syncthreads();
   if (lcnt[t] == 0) st_ext(bucket_slot(buckets, bin, t), ge_identity());
-  for (uint32_t e0 = t; e0 < E; e0 += 256 * SB) {
+#pragma unroll
+  for (int u = 0; u < SORT_REG; ++u)
+    if (reg[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[reg[u].y], 1u)] = reg[u].x;
+  for (uint32_t e0 = t + 256u * SORT_REG; e0 < E; e0 += 256 * SB) {
     uint2 en[SB];
 #pragma unroll
     for (int u = 0; u < SB; ++u) en[u] = e0 + 256u * u < E ? entries[off + e0 + 256u * u] : make_uint2(0u, 0xFFFFFFFFu);
