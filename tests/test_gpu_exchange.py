@@ -97,3 +97,21 @@ def test_exchange_ring_rccl_single_rank(engine, group):
         assert [1 if g else 0 for g in got] == [b["expect_code"] for b in stream]
     finally:
         dist.destroy_process_group()
+
+
+def test_combine_records_device_arguments(engine):
+    """Argument errors are errors, never a verdict: a stride below the 129-byte record, more than
+    4,096 records, a missing or misaligned output."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    d = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    lib, ctx = engine.lib, engine.ctx
+    rec, out = d.data_ptr(), d.data_ptr() + 2048
+    assert lib.edc_combine_records_device(ctx, ctypes.c_void_p(st), 1, ctypes.c_void_p(rec), 128, ctypes.c_void_p(out)) < 0
+    assert lib.edc_combine_records_device(ctx, ctypes.c_void_p(st), 4097, ctypes.c_void_p(rec), 129, ctypes.c_void_p(out)) < 0
+    assert lib.edc_combine_records_device(ctx, ctypes.c_void_p(st), 1, ctypes.c_void_p(rec), 129, None) < 0
+    assert lib.edc_combine_records_device(ctx, ctypes.c_void_p(st), 1, None, 129, ctypes.c_void_p(out)) < 0
+    assert lib.edc_combine_records_device(ctx, ctypes.c_void_p(st), 1, ctypes.c_void_p(rec), 129,
+                                          ctypes.c_void_p(out + 4)) < 0
+    torch.cuda.synchronize()

@@ -177,3 +177,25 @@ def test_two_rank_sharded_fallback(tmp_path, name):
     for r in range(world):
         assert json.load(open(out + f".{r}")) == expect
 
+
+
+def test_exchange_ring_pop_without_post():
+    """ExchangeRing.pop with nothing posted is a usage error, not a hang or a bogus record (a
+    single-rank gloo group on the CPU)."""
+    import torch
+    import torch.distributed as dist
+    import importlib
+    from conftest import load_pkg
+    load_pkg()
+    sharded = importlib.import_module("ed25519_consensus_amd.sharded")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ring = sharded.ExchangeRing(dist, torch.device("cpu"), depth=2, group=2)
+        with pytest.raises(RuntimeError):
+            ring.pop()
+        ring.post(bytes(range(129)))
+        assert ring.pop() == [bytes(range(129))]
+        assert len(ring) == 0
+    finally:
+        dist.destroy_process_group()
