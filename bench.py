@@ -8,9 +8,12 @@ resident in HBM before timing starts. A step = the full hot path: SHA-512 challe
 decompression, key grouping, ChaCha z + scalar coefficients, Pippenger MSM, [8]/identity.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1048576] [--keys 150] [--msg-len 120]
-  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-  (weak scaling: each rank verifies its own 2^20-signature slice of one global batch; the
-   ranks all-gather one 128-byte partial point each over RCCL and combine it.)
+  multi-GPU: python bench.py --gpus N ... starts N ranks itself (torch.distributed.run as a child
+  process, before anything touches the GPU); under an outer torch.distributed.run it is one rank.
+  At N > 1 the headline is the metric's shape, strong scaling: every step is ONE batch of --n
+  (2^20) signatures split over the N ranks; each rank reduces its contiguous shard to one partial
+  point and the ranks all-gather the 129-byte records over RCCL and combine them. The weak shape
+  (--n per rank) is reported beside it as `scaling_other_shape`.
 """
 import argparse
 import ctypes
@@ -146,6 +149,43 @@ def cpu_baseline(vk, sig, msg, off, n_sample, keys, msg_len):
     return oracle_c.baseline_c3(n_sample=n_sample, keys=keys, msg_len=msg_len, data=data)
 
 
+def host_api_leg(eng, vk, sig, msg, off, n, zseed, reps=8):
+    """The synchronous host-buffer calls the Rust shim makes (reference
+    `Verifier::verify`, src/batch.rs:149): the same n items copied once into pageable host memory,
+    then `edc_batch_verify_prehashed` (queued `Item {vk_bytes, sig, k}`, 128 B per item over PCIe,
+    the shim's call) and `edc_batch_verify` (vk, sig and the message arena; SHA-512 on the GPU),
+    each call timed from the host pointers to its verdict. PCIe-inclusive, after the timed region,
+    never the headline `value`."""
+    import numpy as np
+    lib = eng.lib
+    hv = vk[:32 * n].cpu().numpy().tobytes()
+    hs = sig[:64 * n].cpu().numpy().tobytes()
+    ho = (off[:n + 1] - off[0]).cpu().numpy().astype(np.uint64)
+    hm = msg[int(off[0]):int(off[n])].cpu().numpy().tobytes() or b"\0"
+    optr = ho.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+    kb = ctypes.create_string_buffer(32 * max(n, 1))
+    eng._check(lib.edc_challenge(eng.ctx, n, hv, hs, hm, optr, kb))
+    hk = kb.raw
+    out = {"n": n, "reps": reps, "memory": "pageable host buffers (bytes objects), copied by the call"}
+    calls = {"prehashed": lambda: lib.edc_batch_verify_prehashed(eng.ctx, n, hv, hs, hk, zseed, None, None),
+             "with_messages": lambda: lib.edc_batch_verify(eng.ctx, n, hv, hs, hm, optr, zseed, None)}
+    for name, f in calls.items():
+        for _ in range(2):
+            eng._check(f())
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            rc = f()
+            ts.append(time.perf_counter() - t)
+            assert rc == 0, f"host-API {name}: valid batch rejected ({rc})"
+        ts.sort()
+        med = ts[len(ts) // 2]
+        out[name] = {"ms_median": round(med * 1e3, 3), "ms_min": round(ts[0] * 1e3, 3),
+                     "sigs_per_s": round(n / med, 1),
+                     "h2d_bytes": len(hv) + len(hs) + (len(hk) if name == "prehashed" else len(hm) + ho.nbytes)}
+    return out
+
+
 def openssl_anchor(seconds=2, cores=1):
     """SURVEY.md 8(d) / BASELINE.md anchor: `openssl speed ed25519` verify/s on the host. OpenSSL
     verifies one signature at a time under RFC 8032 cofactorless rules (it rejects non-canonical
@@ -171,6 +211,42 @@ def openssl_anchor(seconds=2, cores=1):
             "sample": f"{' '.join(cmd[1:])} ({ver})"}
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, nranks, port):
+    """The child command that runs `nranks` ranks of this script (one process per GPU, RCCL)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, nranks, call=None):
+    """`--gpus N` (N > 1) without an outer torch.distributed.run: start the N ranks as ONE child
+    process before this process imports torch or touches HIP (no exec: the child is waited for).
+    Rank 0 prints the JSON line straight to the inherited stdout; torch.distributed.run exits
+    non-zero when any rank fails, and that code is returned."""
+    import subprocess
+    call = call or subprocess.call
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC only on this pool (RCCL)
+    return call(rank_launch_cmd(argv, nranks, free_port()), env=env)
+
+
+def world_error(gpus, world, backend, local_world, ndev):
+    """Why this rank must not run (None if it may): the process group must be exactly the --gpus
+    ranks asked for, and with RCCL every local rank needs a GPU of its own (the gloo rehearsal
+    shares the visible GPUs on purpose)."""
+    if world != gpus:
+        return f"--gpus {gpus} but the process group has {world} rank(s)"
+    if backend != "gloo" and world > 1 and ndev < local_world:
+        return f"{local_world} ranks on this node but only {ndev} GPU(s) visible"
+    return None
+
+
 CONFIGS = {   # BASELINE.json configs: (items per GPU, validators (0 = distinct keys), message bytes (-1 = 0..1024))
     "c2": (1 << 16, 0, 32, "configs[1]: 2^16 sigs, distinct keys, 32-byte msgs"),
     "c3": (1 << 20, 150, 120, "configs[2]: 2^20 votes/GPU from 150 validators, 120-byte msgs"),
@@ -178,7 +254,7 @@ CONFIGS = {   # BASELINE.json configs: (items per GPU, validators (0 = distinct 
 }
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
@@ -192,15 +268,18 @@ def main():
     ap.add_argument("--msg-len", type=int, default=None, help="message bytes (-1 = uniform 0..1024)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) synchronous calls reported after the timed region")
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU (submit/wait pipelining, <= the context's 16 slots); "
                          "0 = 6 from 2^19 signatures per GPU up, 16 below (small shards need more overlap)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: every rank verifies --n signatures of one global batch; strong: the ranks split "
-                         "one batch of --n signatures (n/G each)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="strong (default at N > 1, the metric's whole-node 2^20 batch): the ranks split one batch "
+                         "of --n signatures (n/N each); weak (N = 1): every rank verifies --n signatures of one "
+                         "global batch")
     ap.add_argument("--window-bits", type=int, default=0, help="Pippenger window width (0 = chosen from the batch size)")
     ap.add_argument("--msm-parts", type=int, default=0, help="MSM parts per batch (0 = chosen from the batch size)")
     ap.add_argument("--bin-entries", type=int, default=0, help="target MSM entries per bin (0 = chosen from the batch size)")
@@ -220,20 +299,32 @@ def main():
     ap.add_argument("--exchange-group", type=int, default=4,
                     help="multi-rank: batches whose records leave in one all-gather (sharded.ExchangeRing)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(sys.argv[1:] if argv is None else argv, args.gpus)
     c_n, c_keys, c_len, c_desc = CONFIGS[args.config]
     args.n = c_n if args.n is None else args.n
     args.keys = c_keys if args.keys is None else args.keys
     args.msg_len = c_len if args.msg_len is None else args.msg_len
 
-    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    if args.scaling is None:
+        args.scaling = "strong" if world > 1 else "weak"
     # EDC_DIST_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing the
     # visible GPUs (the all-gather then goes through host memory); the default is RCCL
     backend = os.environ.get("EDC_DIST_BACKEND", "nccl")
+    import torch
+    # counting devices does not initialise the GPU
+    err = world_error(args.gpus, world, backend, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))),
+                      torch.cuda.device_count())
+    if err:
+        print(f"bench.py rank {rank}: {err}", file=sys.stderr, flush=True)
+        return 2
+    dist = None
     if backend == "gloo":
         local = local % torch.cuda.device_count()
     # EDC_FORCE_DIST=1 (rehearsal only): run the multi-rank path -- process group, per-batch
@@ -241,12 +332,20 @@ def main():
     # one-GPU box; the numbers are not a scaling measurement
     force_dist = os.environ.get("EDC_FORCE_DIST") == "1"
     if world > 1 or force_dist:
+        import datetime
         import torch.distributed as dist
         # RCCL's streams at high priority: the per-group collective must not queue behind the
         # in-flight batches' kernels for a free CU
         os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        # a rank that dies mid-run ends the others' collectives within this bound instead of the
+        # backend's default (10-30 min)
+        dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=120))
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py rank {rank}: --gpus {args.gpus} but the group formed with {dist.get_world_size()} "
+                  "rank(s)", file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            return 2
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     torch.zeros(1, device=dev)                     # initialise torch's HIP runtime first
@@ -422,18 +521,20 @@ def main():
             args.inflight = min(6 if n >= (1 << 19) else small_depth, slots)
             eng._check(lib.edc_set_slots(eng.ctx, args.inflight))
         eng._check(lib.edc_reserve(eng.ctx, n))
-        if n <= n_main:
-            # as many signatures as the headline run (steps x n_main / n): a short run of small
-            # batches is mostly the pipeline's fill and drain (16 batches in flight)
-            k2 = max(args.steps, round(args.steps * n_main / max(1, n)))
-            run_steps(max(2, args.warmup))
-            el2, codes2 = timed(k2)
-            other = {"scaling": "weak" if args.scaling == "strong" else "strong", "sigs_per_gpu": n,
-                     "inflight": args.inflight, "steps": k2,
-                     "value": round(n * world * k2 / el2, 1), "ms_per_step": round(el2 / k2 * 1e3, 3),
-                     "verdict_ok": all(c == 0 for c in codes2)}
-        else:
-            other = {"scaling": "weak", "skipped": "the weak shape needs --n per rank; this rank holds --n / world"}
+        main_data = (vk, sig, msg, off)
+        if n > n_main:      # the weak shape beside a strong headline: --n signatures of this rank's own
+            vk, sig, msg, off = make_workload(pkg, eng, torch, dev, n, args.keys, args.msg_len, base)
+            torch.cuda.synchronize()
+        # as many signatures as the headline run (steps x n_main / n): a short run of small
+        # batches is mostly the pipeline's fill and drain (16 batches in flight)
+        k2 = max(args.steps, round(args.steps * n_main / max(1, n)))
+        run_steps(max(2, args.warmup))
+        el2, codes2 = timed(k2)
+        other = {"scaling": "weak" if args.scaling == "strong" else "strong", "sigs_per_gpu": n,
+                 "inflight": args.inflight, "steps": k2,
+                 "value": round(n * world * k2 / el2, 1), "ms_per_step": round(el2 / k2 * 1e3, 3),
+                 "verdict_ok": all(c == 0 for c in codes2)}
+        vk, sig, msg, off = main_data
         n, base = n_main, base_main
         if args.inflight != inflight_main:
             args.inflight = inflight_main
@@ -519,6 +620,9 @@ def main():
                             "source": "profiles/valu_pmc.json (SQ_INSTS_VALU, SQ_INSTS_VALU_INT64, GRBM_GUI_ACTIVE)"}
             except Exception:
                 valu = None
+        host_api = None
+        if not args.no_host_api and world == 1 and nmb == 1 and hasattr(lib, "edc_batch_verify_prehashed"):
+            host_api = host_api_leg(eng, vk, sig, msg, off, n, zseed)
         cpu = None
         if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
             cpu = cpu_baseline(vk, sig, msg, off, args.cpu_sample, args.keys, args.msg_len)
@@ -569,10 +673,10 @@ def main():
                                        "note": "same kernel inside the in-flight loop: HIP events on its stream, "
                                                "so the duration includes waiting for CUs held by the other "
                                                "in-flight batches (rocprof's begin-to-end average of the "
-                                               "pipelined run is shorter: profiles/r01_kernel_stats_pipelined.csv)"},
+                                               "pipelined run is shorter: profiles/r06/r06_kernel_stats_pipelined.csv)"},
                          "measured": f"HIP events on the slot stream around each launch, {max(1, args.profile_steps)} "
                                      "instrumented batches run one at a time after the timed region "
-                                     "(rocprof cross-check: profiles/r01_kernel_stats_inflight1.csv)"},
+                                     "(rocprof cross-check: profiles/r06/r06_kernel_stats_inflight1.csv)"},
             # k_challenge against its own issue bound: per 128-byte block and lane, 80 rounds of 7
             # v_lshl_add_u64 + 20 32-bit VALU (12 v_alignbit, 8 v_bitop3) and 64 schedule steps of
             # 3 + 14 (ISA of the compression loop, tools: llvm-objdump of libedc.so), priced at the
@@ -603,6 +707,8 @@ def main():
             "phases_ms": phases,
             # one batch alone, start to verdict (sum of the phases of the instrumented batches)
             "batch_latency_ms": round(sum(phases.values()), 3),
+            # the host-buffer synchronous calls of the Rust shim (PCIe included), NOT `value`
+            "host_api": host_api,
             "cpu_baseline": cpu,
             "gen_s": round(t_gen, 2),
         }
@@ -612,7 +718,8 @@ def main():
     eng.close()
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

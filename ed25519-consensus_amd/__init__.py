@@ -252,6 +252,7 @@ class Engine:
         if not self.ctx:
             raise EngineError(f"edc_create({device}) failed")
         self._lock = threading.Lock()
+        self._kc_keys = set()          # host mirror of the key cache's key bytes (keycache_missing)
         self._host_inflight = {}        # ticket -> host buffers borrowed by edc_batch_submit
 
     def close(self):
@@ -455,6 +456,7 @@ class Engine:
         ok = ctypes.create_string_buffer(max(n, 1))
         with self._lock:
             u = self._check(self.lib.edc_keycache_load(self.ctx, n, b"".join(encs) or b"\0", ok))
+            self._kc_keys = set(bytes(e) for e in encs)      # load caches every distinct key
         return u, [bool(b) for b in ok.raw[:n]]
 
     def keycache_add(self, encs):
@@ -465,7 +467,14 @@ class Engine:
         ok = ctypes.create_string_buffer(max(n, 1))
         with self._lock:
             u = self._check(self.lib.edc_keycache_add(self.ctx, n, b"".join(encs) or b"\0", ok))
-        return u, [bool(b) for b in ok.raw[:n]]
+            oks = [bool(b) for b in ok.raw[:n]]
+            self._kc_keys.update(bytes(e) for e, o in zip(encs, oks) if o)   # add keeps decodable keys only
+        return u, oks
+
+    def keycache_missing(self, encs):
+        """The distinct keys of encs that the context's key cache does not hold yet (host-side
+        mirror of the cache's key set, no device call)."""
+        return set(bytes(e) for e in encs) - self._kc_keys
 
     def set_key_grouping(self, mode):
         """0 auto (default), 1 always group keys, 2 never (one A term per signature), 3 test mode:
@@ -488,6 +497,7 @@ class Engine:
     def keycache_clear(self):
         with self._lock:
             self._check(self.lib.edc_keycache_clear(self.ctx))
+            self._kc_keys = set()
 
     def keycache_size(self):
         return int(self.lib.edc_keycache_size(self.ctx))
@@ -715,6 +725,10 @@ class VerificationKey:
     bound. Keys that do not decode are never added (edc_keycache_add)."""
 
     AUTO_CACHE_KEYS = 1024          # 64 MB of comb tables
+    # Cost of the default (keep_decoded=None): a call that adds new keys rebuilds the cache's hash
+    # table, decodes the new keys' comb tables and synchronises every slot of the engine (it may
+    # not run while batches are in flight; it then only validates). Ingesting keys that are
+    # already cached adds nothing.
 
     __slots__ = ("A_bytes", "_engine", "cached")
 
@@ -738,8 +752,8 @@ class VerificationKey:
         vkbs = [k if isinstance(k, VerificationKeyBytes) else VerificationKeyBytes(k) for k in keys]
         eng = engine or default_engine()
         encs = [v.to_bytes() for v in vkbs]
-        if keep_decoded is None:
-            keep_decoded = eng.keycache_size() + len(set(encs)) <= cls.AUTO_CACHE_KEYS
+        if keep_decoded is None:      # keys already cached cost nothing: only new ones count
+            keep_decoded = eng.keycache_size() + len(eng.keycache_missing(encs)) <= cls.AUTO_CACHE_KEYS
         cached = False
         if keep_decoded and encs:
             try:

@@ -747,14 +747,18 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
                     s.slice_T, s.probe_runs ? EDC_PROBE_SKIP : 0, s.timed ? s.ev_acc[0] : nullptr,
                     s.timed ? s.ev_acc[1] : nullptr, latency);
   s.acc_nbin = P.nbin();
-  if (s.timed) {   // the accumulation's entry count, read at the wait without another sync
-    CK(hipMemcpyAsync(s.h_acc, s.offsets + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    CK(hipMemcpyAsync(s.h_acc + 1, s.counts + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
-  }
+  if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_TAIL], st);
   // the final kernel stores the result block to d_out and straight into the pinned h_out
   if (EDC_RUN(128)) launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out, s.h_out);
-  if (s.timed) (void)hipEventRecord(s.ev[PH_N], st);
+  if (s.timed) {
+    (void)hipEventRecord(s.ev[PH_N], st);
+    // the accumulation's entry count (the last bin's offset + count), read at the wait without
+    // another sync; queued after the last phase event so that no phase time includes the copies
+    if (s.acc_nbin) {
+      CK(hipMemcpyAsync(s.h_acc, s.offsets + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      CK(hipMemcpyAsync(s.h_acc + 1, s.counts + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    }
+  }
   CK(hipGetLastError());
   s.pending = true;
   s.probe_runs++;
@@ -1314,9 +1318,20 @@ int edc_combine_records_device(edc_ctx* ctx, void* stream, size_t g, const uint8
                                uint8_t* d_out) {
   if (!ctx || !d_out || (g && !d_records) || stride < 129 || g > 4096) return EDC_ERR_ARG;
   if (!aligned16(d_out)) { ctx->err = "d_out must be 16-byte aligned"; return EDC_ERR_ARG; }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (st) {     // the caller's stream must belong to the context's GPU
+    int sdev = -1;
+    CK(hipStreamGetDevice(st, &sdev));
+    if (sdev != ctx->device) { ctx->err = "stream is not on the context's device"; return EDC_ERR_ARG; }
+  }
+  // the launch needs the context's device current; the caller's current device is restored
+  int prev = -1;
+  CK(hipGetDevice(&prev));
   CK(hipSetDevice(ctx->device));
-  launch_combine_records(reinterpret_cast<hipStream_t>(stream), (uint32_t)g, d_records, (uint32_t)stride, d_out);
-  CK(hipGetLastError());
+  launch_combine_records(st, (uint32_t)g, d_records, (uint32_t)stride, d_out);
+  const hipError_t e = hipGetLastError();
+  (void)hipSetDevice(prev);
+  CK(e);
   return 0;
 }
 
@@ -1837,8 +1852,10 @@ static int kc_append(edc_ctx* ctx, const std::vector<uint32_t>& neww) {
 
 // distinct keys of vk (m x 32 bytes) not yet cached, in first-occurrence order; of[i] = the
 // cache index key i will have
+// (limit: the most keys the cache may then hold; edc_keycache_add checks it after dropping the
+// keys that do not decode instead)
 static int kc_collect(edc_ctx* ctx, size_t m, const uint8_t* vk, std::vector<uint32_t>& of,
-                      std::vector<uint32_t>& neww) {
+                      std::vector<uint32_t>& neww, size_t limit = KC_MAX_KEYS) {
   std::unordered_map<std::string, uint32_t> idx;
   for (uint32_t c = 0; c < ctx->kc_m; ++c)
     idx.emplace(std::string(reinterpret_cast<const char*>(&ctx->kc_words[8 * c]), 32), c);
@@ -1847,7 +1864,7 @@ static int kc_collect(edc_ctx* ctx, size_t m, const uint8_t* vk, std::vector<uin
     auto it = idx.emplace(std::string(reinterpret_cast<const char*>(vk + 32 * i), 32), (uint32_t)idx.size());
     of[i] = it.first->second;
     if (it.second) {
-      if (idx.size() > KC_MAX_KEYS) { ctx->err = "key cache holds at most 65536 keys"; return EDC_ERR_ARG; }
+      if (idx.size() > limit) { ctx->err = "key cache holds at most 65536 keys"; return EDC_ERR_ARG; }
       uint32_t w[8];
       memcpy(w, vk + 32 * i, 32);
       neww.insert(neww.end(), w, w + 8);
@@ -1882,7 +1899,7 @@ int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok)
   int rc = sync_all(ctx);
   if (rc) return rc;
   std::vector<uint32_t> of, words;
-  if ((rc = kc_collect(ctx, m, vk, of, words))) return rc;
+  if ((rc = kc_collect(ctx, m, vk, of, words, SIZE_MAX))) return rc;
   // keys that fail to decode (VerificationKey::try_from's MalformedPublicKey) are not added: the
   // entry is meant for keys parsed from untrusted input, and a malformed one must not pin 64 KB of
   // comb table. of[] is remapped to the kept keys; a dropped key reports ok = 0.
@@ -1911,6 +1928,7 @@ int64_t edc_keycache_add(edc_ctx* ctx, size_t m, const uint8_t* vk, uint8_t* ok)
       remap[j] = u0 + (uint32_t)(keep.size() / 8);
       keep.insert(keep.end(), &words[8 * j], &words[8 * j] + 8);
     }
+  if (u0 + keep.size() / 8 > KC_MAX_KEYS) { ctx->err = "key cache holds at most 65536 keys"; return EDC_ERR_ARG; }
   if ((rc = kc_append(ctx, keep))) return rc;
   if (ok)
     for (size_t i = 0; i < m; ++i) {

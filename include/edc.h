@@ -90,6 +90,9 @@ int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const u
  * ticket and returns its verdict (EDC_OK / EDC_INVALID_SIGNATURE, <0 on runtime failure), with
  * optional check8 (needs want_check8), partial point and bad flag. Tickets must be waited in
  * submission order before their slot is reused; inputs must stay valid until the wait.
+ * Whenever *bad is set (an undecodable R or key, or s >= l in the batch) the partial is the
+ * IDENTITY, not the shard's check point: a caller combining partials must OR the bad flags and
+ * treat a set flag as a rejection (edc_combine_partials' bad_any), never test [8]*partial alone.
  */
 int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                                 const uint8_t* d_msg, const uint64_t* d_msg_off,
@@ -152,8 +155,11 @@ int64_t edc_batch_submit_indexed(edc_ctx* ctx, size_t n, const uint32_t* key_idx
 /*
  * Multi-GPU shard: evaluate this shard's part of the batch equation WITHOUT the cofactor /
  * identity step. partial (128 bytes) = canonical X||Y||Z||T of the shard's check point;
- * *bad = 1 if any item of the shard failed decoding / canonicity. Items are the shard's slice
- * of the global queue starting at global index z_base (device pointers).
+ * *bad = 1 if any item of the shard failed decoding / canonicity, and then the partial is the
+ * IDENTITY (deterministic whatever the addition order; the off-curve sum is not): callers must
+ * check *bad and pass the OR of the shards' flags to edc_combine_partials, whose verdict is then a
+ * rejection. Items are the shard's slice of the global queue starting at global index z_base
+ * (device pointers).
  */
 int edc_batch_partial_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                              const uint8_t* d_msg, const uint64_t* d_msg_off,
@@ -172,7 +178,8 @@ int edc_combine_partials(edc_ctx* ctx, size_t g, const uint8_t* partials, int ba
  * already in this GPU's memory): record r at d_records + r*stride holds a shard's canonical
  * 128-byte partial point followed by its bad byte. The sum, x8 and the identity test (reference
  * src/batch.rs:212-216) run as one small kernel ENQUEUED on the caller's HIP stream `stream`
- * (the stream the all-gather ran on, so no host round trip and no synchronization); the 256-byte
+ * (the stream the all-gather ran on, so no host round trip and no synchronization; it must belong
+ * to ctx's device, else EDC_ERR_ARG; the calling thread's current device is left unchanged); the 256-byte
  * result block lands in d_out (device, 16-byte aligned): int[0] = 0 Ok / 1 reject, int[1] = bad.
  */
 int edc_combine_records_device(edc_ctx* ctx, void* stream, size_t g, const uint8_t* d_records, size_t stride,

@@ -98,6 +98,21 @@ for step in "$@"; do
     lat) run lat 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 ;;
     lat=*) v=${step#lat=}; run lat_$v 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 --lib "$PWD/$D/libedc_$v.so" ;;
     gloo4) run gloo4 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 4 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    # bench.py's own launcher (no outer torch.distributed.run): two gloo ranks sharing the GPU
+    # must run and report n_gpus 2 / comm.world_size 2; two RCCL ranks on a one-GPU box must
+    # refuse within seconds (non-zero exit, expected)
+    launch2g) run launch2g 300 env EDC_DIST_BACKEND=gloo python3 -u bench.py --gpus 2 --steps 4 --warmup 2 --no-cpu-baseline ;;
+    launch2r)
+      t0=$(date +%s.%N)
+      timeout -k 10 120 python3 -u bench.py --gpus 2 --steps 4 > "$(log launch2r)" 2>&1
+      rc=$?; t1=$(date +%s.%N)
+      echo "[launch2r] rc=$rc (expected non-zero) in $(python3 -c "print(round($t1-$t0,1))") s: $(grep -m1 'GPU(s) visible' "$(log launch2r)")" | tee -a "$(log launch2r)"
+      if [ $rc -eq 0 ] || [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit 1; fi ;;
+    # the strong shape's per-rank shard at the driver's run length: 20 steps of 2^20 split over
+    # 8 ranks = 160 batches of 2^17 per GPU (over 4 ranks: 80 of 2^18)
+    n17x160) bench_step n17x160 --n 131072 --steps 160 --warmup 5 --no-cpu-baseline --no-host-api ;;
+    n18x80) bench_step n18x80 --n 262144 --steps 80 --warmup 5 --no-cpu-baseline --no-host-api ;;
+    n17x20) bench_step n17x20 --n 131072 --steps 20 --warmup 5 --no-cpu-baseline --no-host-api ;;
     ab=*)
       IFS=, read -ra libs <<< "${step#ab=}"
       for rep in $(seq 1 "${AB_REPS:-2}"); do
