@@ -4,6 +4,8 @@
 #include <string.h>
 #include <string>
 #include <random>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -180,6 +182,10 @@ struct edc_ctx {
   uint32_t last_uncached = 0;
   int multi_union = 1;                  // edc_set_multi_union
   uint64_t mu_hits = 0, mu_reruns = 0;  // union-first launches that passed / were rerun per batch
+  // chunked synchronous host-buffer calls (run_host_chunked): a copy stream and one event per
+  // chunk (+ the keys / offsets piece), created on first use
+  hipStream_t hcs = nullptr;
+  hipEvent_t hev[9] = {};
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
     if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, 0, 0};
@@ -1010,6 +1016,233 @@ static int run_batch_sync(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uin
   return finish_batch(ctx, s, check8, partial, bad);
 }
 
+// ---- synchronous host-buffer calls, copy overlapped with compute ----
+// A host-buffer call (the Rust shim's Verifier::verify, src/batch.rs:149) used to copy every input
+// over PCIe and only then start the pipeline: at 2^20 prehashed items 134 MB (~2.5 ms at ~53 GB/s)
+// + ~1.6 ms of compute. Here the inputs travel in pieces on a copy stream and each piece's work
+// starts as it lands: the keys (and message offsets / caller z) first, so the key grouping and the
+// keys' decode run under the signature copy; then the signatures (+ k or the message bytes) in
+// chunks, each followed by its R decode (second stream) and its SHA-512 + coefficient pass (slot
+// stream). A copy from pageable memory returns only when it has landed, so the calling thread
+// issues nothing but copies and events, back to back, while a launcher thread enqueues each
+// piece's kernels behind its event. The last chunk is small, so that little remains after the
+// last byte: its decode and coefficients, the per-key merge, binning, sort and the MSM. Same
+// kernels, same per-item / per-key arithmetic and the same integer sums (order-independent), so
+// verdict and [8]*check are bit-identical to the one-piece path (tests/test_gpu_hostchunk.py).
+constexpr size_t kHostChunkMin = 1u << 16;   // smaller calls copy in one piece (latency-bound anyway)
+constexpr int kHostChunks = 8;               // chunks of signatures (ctx->hev: one event each + piece 0)
+
+static bool host_chunked_ok(const edc_ctx* ctx, size_t n) {
+  static const bool off = getenv("EDC_HOST_CHUNKS") && getenv("EDC_HOST_CHUNKS")[0] == '0';   // A/B measurement
+  return !off && n >= kHostChunkMin && n < (1ull << 28) && !ctx->timing && ctx->slot[0].st2;
+}
+
+// chunk boundaries: kHostChunks - 1 equal chunks, then a last one of ~n/32; every boundary but n
+// is a multiple of COEF_CHUNK (k_coef's workgroups start on one)
+static std::vector<size_t> host_chunks(size_t n) {
+  const size_t last = ((n + 31) / 32 + COEF_CHUNK - 1) / COEF_CHUNK * COEF_CHUNK;
+  const size_t body = n > last ? (n - last) / COEF_CHUNK * COEF_CHUNK : 0;
+  // body chunks of ~2^18 items: every pageable copy costs ~20-25 us of host time before the next
+  // can start (r06c/r06d traces), and a 2^18 decode still ends under the next chunk's copy
+  static const int env_chunks = getenv("EDC_HOST_BODY_CHUNKS") ? atoi(getenv("EDC_HOST_BODY_CHUNKS")) : 0;
+  size_t k = env_chunks > 0 ? (size_t)env_chunks : (body + (1u << 17)) >> 18;
+  if (k < 1) k = 1;
+  if (k > kHostChunks - 1) k = kHostChunks - 1;
+  const size_t c = ((body + k - 1) / k + COEF_CHUNK - 1) / COEF_CHUNK * COEF_CHUNK;
+  std::vector<size_t> b{0};
+  while (b.back() < body && c) b.push_back(b.back() + c < body ? b.back() + c : body);
+  if (b.back() < n) b.push_back(n);
+  return b;
+}
+
+// pieces landed so far (the copying thread counts up, the launcher thread waits)
+struct HostGate {
+  std::mutex m;
+  std::condition_variable cv;
+  int landed = 0;
+  bool abort = false;
+  void post(int k) {
+    { std::lock_guard<std::mutex> g(m); landed = k; }
+    cv.notify_all();
+  }
+  void stop() {
+    { std::lock_guard<std::mutex> g(m); abort = true; }
+    cv.notify_all();
+  }
+  bool wait(int k) {            // false: the copying thread gave up
+    std::unique_lock<std::mutex> g(m);
+    cv.wait(g, [&] { return landed >= k || abort; });
+    return landed >= k;
+  }
+};
+
+// Enqueue the whole chunked batch on slot 0 (inputs in host memory; k: prehashed challenges or
+// null for the message path; z: caller-drawn z or null for the seed). The host buffers and
+// `rebased` are read by the copies until the slot's wait.
+static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                                const uint64_t* msg_off, const uint8_t* k, const uint8_t* z, const uint8_t* z_seed,
+                                int want_compress, std::vector<uint64_t>& rebased) {
+  Slot& s = ctx->slot[0];
+  const size_t mbytes = k ? 0 : (size_t)(msg_off[n] - msg_off[0]);
+  int rc = ensure_n(ctx, n);
+  if (!rc) rc = ensure_slot(ctx, s, n);
+  if (!rc && !k) rc = ensure_msg(ctx, mbytes);
+  if (rc) return rc;
+  if (!ctx->hcs) {
+    CK(hipStreamCreateWithFlags(&ctx->hcs, hipStreamNonBlocking));
+    for (hipEvent_t& e : ctx->hev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const bool per_sig = choose_per_sig(ctx, n), split = choose_split(ctx);
+  const MsmPlan P = batch_plan(ctx, n, per_sig, split);
+  rc = ensure_msm(ctx, s, P, split ? msm_entry_capacity(P, 2 + 3 * n, 0) : msm_entry_capacity(P, n, n + 1));
+  if (rc) return rc;
+  const uint32_t N = (uint32_t)n;
+  const uint32_t T = (uint32_t)next_pow2(2 * (n < 128 ? 128 : n));
+  if (T > s.cap_T) { ctx->err = "hash table capacity"; return EDC_ERR_ARG; }
+  uint32_t seed[8];
+  seed_words(z_seed, seed);
+  hipStream_t st = s.st, st2 = s.st2, cs = ctx->hcs;
+  s.kin = s.k;
+  s.nmulti = 0;
+  s.timed = false;
+  s.per_sig = per_sig;
+  s.n_batch = N;
+  const std::vector<size_t> cb = host_chunks(n);
+  const int nchunks = (int)cb.size() - 1;
+  if (!k && msg_off[0] != 0) {
+    rebased.resize(n + 1);
+    for (size_t i = 0; i <= n; ++i) rebased[i] = msg_off[i] - msg_off[0];
+  }
+  const uint64_t salt64 = per_sig ? 0 : splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
+  const KeyCacheView kc = ctx->kc();
+
+  // the launcher thread: every kernel, each piece's behind that piece's event
+  HostGate gate;
+  std::string lerr;
+  int lrc = 0;
+  std::thread launcher([&] {
+    auto fail = [&](const char* what, hipError_t e) {
+      (void)hipGetLastError();
+      lerr = std::string(what) + ": " + hipGetErrorString(e);
+      lrc = EDC_ERR_HIP;
+    };
+#define LK(expr)                                   \
+  do {                                             \
+    hipError_t e_ = (expr);                        \
+    if (e_ != hipSuccess) return fail(#expr, e_);  \
+  } while (0)
+    LK(hipSetDevice(ctx->device));
+    launch_init_batch(st, s.flags, per_sig ? (int)N : -1, s.u_acc, s.d_out, per_sig ? nullptr : s.table,
+                      per_sig ? 0u : T, s.counts, P.nbin());
+    if (!gate.wait(1)) return;
+    LK(hipStreamWaitEvent(st, ctx->hev[0], 0));
+    if (!per_sig) {
+      const uint32_t salt[2] = {(uint32_t)salt64, (uint32_t)(salt64 >> 32)};
+      launch_keys(st, N, ctx->vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
+                  s.key_index, s.key_acc, s.flags);
+    }
+    LK(hipEventRecord(s.ev_keys, st));
+    LK(hipStreamWaitEvent(st2, s.ev_keys, 0));
+    launch_decompress_range(st2, N, 0, 0, true, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n,
+                            s.keybad, s.flags, kc, split);
+    for (int c = 0; c < nchunks; ++c) {
+      const size_t c0 = cb[c], cnt = cb[c + 1] - cb[c];
+      if (!gate.wait(c + 2)) return;
+      hipEvent_t ev = ctx->hev[c + 1];
+      LK(hipStreamWaitEvent(st2, ev, 0));
+      launch_decompress_range(st2, N, (uint32_t)c0, (uint32_t)cnt, false, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts,
+                              s.itembad + s.cap_n, s.keybad, s.flags, kc, split);
+      LK(hipStreamWaitEvent(st, ev, 0));
+      if (!k)
+        launch_challenge(st, (uint32_t)cnt, ctx->vk + c0 * 32, ctx->sig + c0 * 64, ctx->msg, ctx->off + c0,
+                         s.k + c0 * 8);
+      launch_coef_range(st, N, (uint32_t)c0, (uint32_t)cnt, ctx->sig, s.k, z ? ctx->zexp : nullptr, seed, 0,
+                        s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags, per_sig, s.coef_part, split);
+    }
+    LK(hipEventRecord(s.ev_dec, st2));
+    launch_coef_finish(st, N, s.key_acc, s.u_acc, s.scal, s.flags, per_sig, s.coef_part, split);
+    launch_msm_bin(st, P, batch_terms(P, s, N, split), split ? 2 + 3 * N : 1 + 2 * N, s.counts, s.offsets, s.cursor,
+                   s.entries, s.flags, true);
+    launch_msm_sort(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.buckets);
+    LK(hipStreamWaitEvent(st, s.ev_dec, 0));
+    launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads,
+                      s.slice_W, s.slice_T, 0, nullptr, nullptr, true);
+    launch_msm_tail(st, P, s.slice_W, s.slice_T, s.win, s.flags, want_compress, s.d_out, s.h_out);
+    LK(hipGetLastError());
+#undef LK
+  });
+
+  // this thread: the copies, back to back, one event per piece
+  auto copies = [&]() -> int {
+    CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, cs));
+    if (!k)
+      CK(hipMemcpyAsync(ctx->off, rebased.empty() ? msg_off : rebased.data(), (n + 1) * sizeof(uint64_t),
+                        hipMemcpyHostToDevice, cs));
+    if (z) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, cs));
+    CK(hipEventRecord(ctx->hev[0], cs));
+    gate.post(1);
+    for (int c = 0; c < nchunks; ++c) {
+      const size_t c0 = cb[c], cnt = cb[c + 1] - cb[c];
+      CK(hipMemcpyAsync(ctx->sig + c0 * 64, sig + c0 * 64, cnt * 64, hipMemcpyHostToDevice, cs));
+      if (k) {
+        CK(hipMemcpyAsync(s.k + c0 * 8, k + c0 * 32, cnt * 32, hipMemcpyHostToDevice, cs));
+      } else {
+        const size_t b0 = (size_t)(msg_off[c0] - msg_off[0]), b1 = (size_t)(msg_off[c0 + cnt] - msg_off[0]);
+        if (b1 > b0) CK(hipMemcpyAsync(ctx->msg + b0, msg + msg_off[c0], b1 - b0, hipMemcpyHostToDevice, cs));
+      }
+      CK(hipEventRecord(ctx->hev[c + 1], cs));
+      gate.post(c + 2);
+    }
+    return 0;
+  };
+  rc = copies();
+  if (rc) gate.stop();
+  launcher.join();
+  if (rc) return rc;
+  if (lrc) { ctx->err = lerr; return lrc; }
+  s.acc_nbin = P.nbin();
+  s.pending = true;
+  return 0;
+}
+
+// One synchronous batch from host buffers, chunked when it pays (see above), else staged in one
+// piece and run by run_batch_sync.
+static int run_host_sync(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
+                         const uint64_t* msg_off, const uint8_t* k, const uint8_t* z, const uint8_t* z_seed,
+                         uint8_t check8[32]) {
+  Slot& s = ctx->slot[0];
+  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
+  if (n && (!vk || !sig || (k ? false : !msg_off))) { ctx->err = "null input"; return EDC_ERR_ARG; }
+  if (n && !k && msg_off[n] > msg_off[0] && !msg) { ctx->err = "null msg"; return EDC_ERR_ARG; }
+  if (!host_chunked_ok(ctx, n)) {
+    int rc = init_slot(ctx, s);
+    if (rc) return rc;
+    if (k) {
+      if ((rc = ensure_n(ctx, n)) || (rc = ensure_slot(ctx, s, n))) return rc;
+      if (n) {
+        CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, ctx->st()));
+        CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, ctx->st()));
+        CK(hipMemcpyAsync(s.k, k, n * 32, hipMemcpyHostToDevice, ctx->st()));
+      }
+    } else if ((rc = upload(ctx, n, vk, sig, msg, msg_off))) {
+      return rc;
+    }
+    if (z && n) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, ctx->st()));
+    return run_batch_sync(ctx, n, ctx->vk, ctx->sig, k ? nullptr : ctx->msg, k ? nullptr : ctx->off,
+                          z ? nullptr : z_seed, 0, z ? ctx->zexp : nullptr, check8, nullptr, nullptr, k ? s.k : nullptr);
+  }
+  std::vector<uint64_t> rebased;
+  const int rc = enqueue_host_chunked(ctx, n, vk, sig, msg, msg_off, k, z, z_seed, check8 != nullptr, rebased);
+  if (rc) {     // nothing may still read the staging buffers or the caller's memory
+    (void)hipStreamSynchronize(ctx->hcs);
+    (void)hipStreamSynchronize(s.st2);
+    (void)hipStreamSynchronize(s.st);
+    s.pending = false;
+    return rc;
+  }
+  return finish_batch(ctx, s, check8, nullptr, nullptr);
+}
+
 extern "C" {
 
 int edc_device_count(void) {
@@ -1107,6 +1340,10 @@ void edc_destroy(edc_ctx* ctx) {
       if (e) (void)hipEventDestroy(e);
     if (s.st) (void)hipStreamDestroy(s.st);
   }
+  if (ctx->hcs) (void)hipStreamSynchronize(ctx->hcs);
+  for (hipEvent_t e : ctx->hev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->hcs) (void)hipStreamDestroy(ctx->hcs);
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
                   ctx->btab, ctx->comb_in, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal, ctx->fb_rv, ctx->fb_idx,
                   ctx->fb_g};
@@ -1121,20 +1358,14 @@ int edc_batch_verify(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* s
                      const uint64_t* msg_off, const uint8_t z_seed[32], uint8_t check8[32]) {
   if (!ctx || !z_seed) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  int rc = upload(ctx, n, vk, sig, msg, msg_off);
-  if (rc) return rc;
-  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, z_seed, 0, nullptr, check8, nullptr, nullptr);
+  return run_host_sync(ctx, n, vk, sig, msg, msg_off, nullptr, nullptr, z_seed, check8);
 }
 
 int edc_batch_verify_z(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig, const uint8_t* msg,
                        const uint64_t* msg_off, const uint8_t* z, uint8_t check8[32]) {
   if (!ctx || (n && !z)) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  int rc = upload(ctx, n, vk, sig, msg, msg_off);
-  if (rc) return rc;
-  if (n) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, ctx->st()));
-  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, ctx->msg, ctx->off, nullptr, 0, ctx->zexp, check8, nullptr,
-                        nullptr);
+  return run_host_sync(ctx, n, vk, sig, msg, msg_off, nullptr, n ? z : nullptr, nullptr, check8);
 }
 
 int edc_batch_verify_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
@@ -1610,21 +1841,11 @@ int edc_batch_verify_prehashed(edc_ctx* ctx, size_t n, const uint8_t* vk, const 
                                const uint8_t z_seed[32], const uint8_t* z, uint8_t check8[32]) {
   if (!ctx || (!z_seed && !z) || (n && (!vk || !sig || !k || (!z_seed && !z)))) return EDC_ERR_ARG;
   CK(hipSetDevice(ctx->device));
-  Slot& s = ctx->slot[0];
-  if (s.pending) { ctx->err = "slot 0 busy: wait for submitted batches first"; return EDC_ERR_ARG; }
-  int rc = ensure_n(ctx, n);
-  if (rc) return rc;
-  rc = ensure_slot(ctx, s, n);
-  if (rc) return rc;
-  hipStream_t st = ctx->st();
-  if (n) {
-    CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(ctx->sig, sig, n * 64, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(s.k, k, n * 32, hipMemcpyHostToDevice, st));
-    if (z) CK(hipMemcpyAsync(ctx->zexp, z, n * 16, hipMemcpyHostToDevice, st));
+  if (!n) {     // empty batch: Ok through the one-piece path (no input is read)
+    static const uint8_t none[1] = {0};
+    return run_host_sync(ctx, 0, none, none, nullptr, nullptr, none, nullptr, z ? nullptr : z_seed, check8);
   }
-  return run_batch_sync(ctx, n, ctx->vk, ctx->sig, nullptr, nullptr, z ? nullptr : z_seed, 0, z ? ctx->zexp : nullptr,
-                        check8, nullptr, nullptr, s.k);
+  return run_host_sync(ctx, n, vk, sig, nullptr, nullptr, k, z, z_seed, check8);
 }
 
 int edc_batch_verify_prehashed_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,

@@ -12,6 +12,10 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
                        const KeyCacheView& kc, bool split = false);
+// R of items [r0, r0 + rcnt) of an n-item batch, and the distinct keys when `keys`
+void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, bool keys, const uint8_t* sig,
+                             const uint8_t* vk, const uint32_t* key_rep, bool per_sig, uint32_t* pts, uint8_t* itembad,
+                             uint8_t* keybad, int* flags, const KeyCacheView& kc, bool split = false);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
                  uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags,
@@ -21,6 +25,15 @@ void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t*
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
                  bool per_sig, uint32_t* coef_part, bool split = false);
+// launch_coef in pieces (chunked host-buffer calls): the per-item pass over items
+// [item0, item0 + cnt) (item0 a multiple of COEF_CHUNK) as each chunk lands, then once the
+// per-key merge and the coefficient reduction
+void launch_coef_range(hipStream_t st, uint32_t n, uint32_t item0, uint32_t cnt, const uint8_t* sig, const uint32_t* k,
+                       const uint8_t* zexp, const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index,
+                       uint32_t* scal, unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad,
+                       int* flags, bool per_sig, uint32_t* coef_part, bool split = false);
+void launch_coef_finish(hipStream_t st, uint32_t n, unsigned long long* key_acc, unsigned long long* u_acc,
+                        uint32_t* scal, int* flags, bool per_sig, uint32_t* coef_part, bool split = false);
 // words of k_coef's per-workgroup key-slot dump for batches of up to cap_n signatures
 size_t coef_part_words(size_t cap_n);
 // grouped fallback: per-(range, key) / per-range coefficients as listed MSM terms

@@ -215,15 +215,20 @@ __device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
   return ge_to_niels_affine(A);
 }
 
-__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t* __restrict__ sig,
+// n: the batch's items (key points sit at 1 + n + j); this launch decodes R of items
+// [r0, r0 + rcnt) and, with `keys`, the distinct keys (a chunked host-buffer call decodes each
+// chunk's R as it lands and the keys once the key grouping is done).
+__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, uint32_t rcnt, int keys,
+                                                       const uint8_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep, int per_sig_host,
                                                        uint32_t* __restrict__ pts, uint8_t* __restrict__ itembad_r,
                                                        uint8_t* __restrict__ keybad, int* __restrict__ flags,
                                                        KeyCacheView kcache, int split) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t w[8];
-  if (i < n) {
+  if (lane < rcnt) {
+    const uint32_t i = r0 + lane;
     ld_words8(sig + (size_t)i * 64, w);
     ge_p3 P;
     const bool ok = ge_decompress(w, P);
@@ -232,8 +237,9 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, const uint8_t
     if (!ok) atomicOr(&flags[FLAG_BAD], 1);
     return;
   }
-  const uint32_t kbase = (n + 63u) & ~63u;   // key lanes start on a wave boundary (no R/key divergence)
-  if (i < kbase) return;
+  const uint32_t kbase = (rcnt + 63u) & ~63u;   // key lanes start on a wave boundary (no R/key divergence)
+  if (!keys || lane < kbase) return;
+  const uint32_t i = lane;
   const uint32_t j = i - kbase;
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
   if (j >= m) return;
@@ -432,7 +438,8 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               unsigned long long* __restrict__ u_acc,
                                               uint8_t* __restrict__ itembad,
                                               int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m,
-                                              uint32_t* __restrict__ coef_part, int split) {
+                                              uint32_t* __restrict__ coef_part, int split, uint32_t item0,
+                                              uint32_t iend) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
@@ -447,18 +454,22 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
 #pragma unroll
   for (int j = 0; j < PL; ++j) ua[j] = 0;
   bool bad = false, karg = false;
-  const uint32_t base = blockIdx.x * COEF_CHUNK;
+  // items [item0, iend) of the n-item batch (item0 a multiple of COEF_CHUNK: a chunked host-buffer
+  // call launches one range per chunk as it lands; workgroup wg's slot dump sits at its place in
+  // the whole batch's layout)
+  const uint32_t wg = item0 / COEF_CHUNK + blockIdx.x, nwg = (n + COEF_CHUNK - 1) / COEF_CHUNK;
+  const uint32_t base = wg * COEF_CHUNK;
   const uint32_t pair0 = rsize ? (base / rsize) * m : 0u;
   for (int grp = 0; grp < COEF_SIGS_PER_THREAD / 4; ++grp) {
     const uint32_t i0 = base + 4 * (threadIdx.x + 256 * grp);
-    if (i0 >= n) break;
+    if (i0 >= iend) break;
     uint32_t blk[16];
     const bool aligned = ((zbase + i0) & 3) == 0;
     if (!zexp && aligned) chacha20_block(seed.w, (zbase + i0) >> 2, blk);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t i = i0 + q;
-      if (i >= n) break;
+      if (i >= iend) break;
       uint32_t z[4];
       if (zexp) {
         const uint4 zz = *reinterpret_cast<const uint4*>(zexp + (size_t)i * 16);
@@ -543,8 +554,8 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
     // batch mode: this workgroup's key slots go out as plain stores, merged per slot by
     // k_coef_merge (a few validators' sums hit by every workgroup made the global atomics
     // serialize: 0.09 of the 0.17 ms of this phase at 2^20 votes from 150 keys)
-    uint32_t* ptag = coef_part + (size_t)blockIdx.x * COEF_SLOTS;
-    unsigned long long* psum = coef_part_sums(coef_part, gridDim.x) + (size_t)blockIdx.x * COEF_SLOTS * PL;
+    uint32_t* ptag = coef_part + (size_t)wg * COEF_SLOTS;
+    unsigned long long* psum = coef_part_sums(coef_part, nwg) + (size_t)wg * COEF_SLOTS * PL;
     for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
       ptag[s] = tag[s];
       if (tag[s] != 0xFFFFFFFFu) {
@@ -742,19 +753,23 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
   if (n)
     hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, SHA_THREADS)), dim3(SHA_THREADS), 0, st, n, vk, sig, msg, off, k);
 }
-void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
-                       bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
-                       const KeyCacheView& kc, bool split) {
-  // lanes [0, n) decode R_i; the key lanes start at the next wave boundary and cover the largest
+void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, bool keys, const uint8_t* sig,
+                             const uint8_t* vk, const uint32_t* key_rep, bool per_sig, uint32_t* pts, uint8_t* itembad,
+                             uint8_t* keybad, int* flags, const KeyCacheView& kc, bool split) {
+  // lanes [0, rcnt) decode R; the key lanes start at the next wave boundary and cover the largest
   // possible key count (m <= n). A wave holding both would run both decodes one after the other,
   // which doubles a small batch's decode latency. Small launches use one wave per workgroup so
   // that the waves spread over CUs instead of sharing SIMDs.
-  if (n) {
-    const uint64_t lanes = ((n + 63ull) & ~63ull) + n;
-    const uint32_t block = lanes <= 16384 ? 64 : 256;
-    hipLaunchKernelGGL(k_decompress, dim3(cdiv(lanes, block)), dim3(block), 0, st, n, sig, vk, key_rep,
-                       per_sig ? 1 : 0, pts, itembad, keybad, flags, kc, split ? 1 : 0);
-  }
+  const uint64_t lanes = ((rcnt + 63ull) & ~63ull) + (keys ? n : 0u);
+  if (!n || !lanes) return;
+  const uint32_t block = lanes <= 16384 ? 64 : 256;
+  hipLaunchKernelGGL(k_decompress, dim3(cdiv(lanes, block)), dim3(block), 0, st, n, r0, rcnt, keys ? 1 : 0, sig, vk,
+                     key_rep, per_sig ? 1 : 0, pts, itembad, keybad, flags, kc, split ? 1 : 0);
+}
+void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
+                       bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
+                       const KeyCacheView& kc, bool split) {
+  launch_decompress_range(st, n, 0, n, true, sig, vk, key_rep, per_sig, pts, itembad, keybad, flags, kc, split);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
@@ -803,9 +818,25 @@ void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t*
     const uint32_t nwg = cdiv(n, COEF_CHUNK);
     uint32_t* part = per_sig ? nullptr : coef_part;
     hipLaunchKernelGGL(k_coef, dim3(nwg), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index, scal, key_acc,
-                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part, split ? 1 : 0);
-    if (part) hipLaunchKernelGGL(k_coef_merge, dim3(COEF_SLOTS), dim3(256), 0, st, nwg, part, key_acc);
+                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part, split ? 1 : 0, 0u, n);
   }
+  launch_coef_finish(st, n, key_acc, u_acc, scal, flags, per_sig, coef_part, split);
+}
+void launch_coef_range(hipStream_t st, uint32_t n, uint32_t item0, uint32_t cnt, const uint8_t* sig, const uint32_t* k,
+                       const uint8_t* zexp, const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index,
+                       uint32_t* scal, unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad,
+                       int* flags, bool per_sig, uint32_t* coef_part, bool split) {
+  seed8 s;
+  for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
+  if (cnt)
+    hipLaunchKernelGGL(k_coef, dim3(cdiv(cnt, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index,
+                       scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, per_sig ? nullptr : coef_part,
+                       split ? 1 : 0, item0, item0 + cnt);
+}
+void launch_coef_finish(hipStream_t st, uint32_t n, unsigned long long* key_acc, unsigned long long* u_acc,
+                        uint32_t* scal, int* flags, bool per_sig, uint32_t* coef_part, bool split) {
+  if (n && !per_sig)
+    hipLaunchKernelGGL(k_coef_merge, dim3(COEF_SLOTS), dim3(256), 0, st, cdiv(n, COEF_CHUNK), coef_part, key_acc);
   hipLaunchKernelGGL(k_key_final, dim3(grid_cap(cdiv(n > 0 ? n : 1, 256), 1024)), dim3(256), 0, st, n, key_acc,
                      u_acc, scal, flags, per_sig ? 1 : 0, split ? 1 : 0);
 }
@@ -826,7 +857,7 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
                        key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm,
-                       (uint32_t*)nullptr, 0);
+                       (uint32_t*)nullptr, 0, 0u, n);
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }
@@ -841,7 +872,7 @@ void launch_multi_coef(hipStream_t st, uint32_t n, uint32_t nr, uint32_t kstride
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, (const uint8_t*)nullptr, s, zbase,
                        key_index, scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, n / nr, kstride,
-                       (uint32_t*)nullptr, 0);
+                       (uint32_t*)nullptr, 0, 0u, n);
   hipLaunchKernelGGL(k_multi_terms, dim3(grid_cap(cdiv((uint64_t)nr * (per_sig ? 1 : kstride + 1), 256), 1024)),
                      dim3(256), 0, st, n, nr, kstride, key_acc, u_acc, flags, per_sig ? 1 : 0, xpt, xrg, xscal);
 }

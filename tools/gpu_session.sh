@@ -113,6 +113,13 @@ for step in "$@"; do
     n17x160) bench_step n17x160 --n 131072 --steps 160 --warmup 5 --no-cpu-baseline --no-host-api ;;
     n18x80) bench_step n18x80 --n 262144 --steps 80 --warmup 5 --no-cpu-baseline --no-host-api ;;
     n17x20) bench_step n17x20 --n 131072 --steps 20 --warmup 5 --no-cpu-baseline --no-host-api ;;
+    # host-buffer synchronous calls (bench.py's host_api leg): chunked (default) and one piece
+    hapi) run hapi 300 python3 -u bench.py --steps 10 --warmup 3 --no-cpu-baseline
+          python3 -c "import json,sys; d=json.loads(open('$(log hapi)').read().strip().splitlines()[-1]); print('hapi', json.dumps(d['host_api']))" | tee -a "gpurun_out/${tag}_summary.log" ;;
+    hapi=*) v=${step#hapi=}; run hapi_$v 300 env EDC_HOST_BODY_CHUNKS=$v python3 -u bench.py --steps 10 --warmup 3 --no-cpu-baseline
+          python3 -c "import json,sys; d=json.loads(open('$(log hapi_$v)').read().strip().splitlines()[-1]); print('hapi=$v', json.dumps(d['host_api']))" | tee -a "gpurun_out/${tag}_summary.log" ;;
+    hapi0) run hapi0 300 env EDC_HOST_CHUNKS=0 python3 -u bench.py --steps 10 --warmup 3 --no-cpu-baseline
+          python3 -c "import json,sys; d=json.loads(open('$(log hapi0)').read().strip().splitlines()[-1]); print('hapi0', json.dumps(d['host_api']))" | tee -a "gpurun_out/${tag}_summary.log" ;;
     ab=*)
       IFS=, read -ra libs <<< "${step#ab=}"
       for rep in $(seq 1 "${AB_REPS:-2}"); do
