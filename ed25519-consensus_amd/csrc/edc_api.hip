@@ -647,6 +647,18 @@ static bool choose_per_sig(const edc_ctx* ctx, size_t n) {
                                     ctx->last_key_ratio > 0.5 && ctx->ungrouped_run < 7);
 }
 
+// Key lanes of a batch's decode launch. The distinct-key count m is only known on the device, so
+// every possible key (m <= n) used to get a lane: at 2^20 votes from 150 validators, 2^20 lanes
+// (16,384 waves) that exit at once. Grouped batches now get twice the previous grouped batch's key
+// count (at least 4,096 lanes); a batch with more keys loops over them (k_decompress), so the
+// hint only affects speed. One key term per signature: m = n exactly.
+static uint32_t key_lanes(const edc_ctx* ctx, size_t n, bool per_sig) {
+  if (per_sig || !ctx->have_key_ratio) return (uint32_t)n;
+  const double m2 = 2.0 * ctx->last_key_ratio * (double)n;
+  const size_t lanes = m2 < 4096.0 ? 4096 : (size_t)m2 + 64;
+  return (uint32_t)(lanes < n ? lanes : n);
+}
+
 // Enqueue the per-signature prefix of the pipeline on slot s: key grouping, SHA-512 challenges,
 // z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization. With d_k (the
 // prehashed entries: the caller's queue-time k, src/batch.rs:76-94) SHA-512 is skipped and the
@@ -708,7 +720,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
     CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
     if (EDC_RUN(16))
       launch_decompress(s.st2, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags,
-                        ctx->kc(), split);
+                        ctx->kc(), split, key_lanes(ctx, n, per_sig));
     CK(hipEventRecord(s.ev_dec, s.st2));
   }
   mark(PH_COEF);
@@ -728,7 +740,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   if (dual) CK(hipStreamWaitEvent(st, s.ev_dec, 0));
   else if (EDC_RUN(16))
     launch_decompress(st, N, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
-                      split);
+                      split, key_lanes(ctx, n, per_sig));
   CK(hipGetLastError());
   return 0;
 }
@@ -861,7 +873,7 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
     CK(hipEventRecord(s.ev_keys, st));
     CK(hipStreamWaitEvent(s.st2, s.ev_keys, 0));
     launch_decompress(s.st2, n, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
-                      false);
+                      false, key_lanes(ctx, N, per_sig));
     CK(hipEventRecord(s.ev_dec, s.st2));
   }
   launch_multi_coef(st, n, nb, kstride, per_sig, d_sig, s.kin, seed, z_base, s.key_index, s.scal, s.mb_acc, s.u_acc,
@@ -872,7 +884,7 @@ static int enqueue_multi(edc_ctx* ctx, Slot& s, uint32_t nb, size_t n_per, const
   if (dual) CK(hipStreamWaitEvent(st, s.ev_dec, 0));
   else
     launch_decompress(st, n, d_sig, d_vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n, s.keybad, s.flags, ctx->kc(),
-                      false);
+                      false, key_lanes(ctx, N, per_sig));
   CK(hipMemsetAsync(s.mb_bad, 0, nb, st));
   launch_range_prebad(st, n, (uint32_t)n_per, s.itembad, s.itembad + s.cap_n, s.keybad, s.key_index, per_sig, s.mb_bad,
                       s.flags);
@@ -1143,14 +1155,14 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
     }
     LK(hipEventRecord(s.ev_keys, st));
     LK(hipStreamWaitEvent(st2, s.ev_keys, 0));
-    launch_decompress_range(st2, N, 0, 0, true, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts, s.itembad + s.cap_n,
-                            s.keybad, s.flags, kc, split);
+    launch_decompress_range(st2, N, 0, 0, key_lanes(ctx, n, per_sig), ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts,
+                            s.itembad + s.cap_n, s.keybad, s.flags, kc, split);
     for (int c = 0; c < nchunks; ++c) {
       const size_t c0 = cb[c], cnt = cb[c + 1] - cb[c];
       if (!gate.wait(c + 2)) return;
       hipEvent_t ev = ctx->hev[c + 1];
       LK(hipStreamWaitEvent(st2, ev, 0));
-      launch_decompress_range(st2, N, (uint32_t)c0, (uint32_t)cnt, false, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts,
+      launch_decompress_range(st2, N, (uint32_t)c0, (uint32_t)cnt, 0, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts,
                               s.itembad + s.cap_n, s.keybad, s.flags, kc, split);
       LK(hipStreamWaitEvent(st, ev, 0));
       if (!k)

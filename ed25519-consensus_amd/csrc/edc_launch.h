@@ -11,9 +11,10 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
                       const uint8_t* msg, const uint64_t* off, uint32_t* k);
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
-                       const KeyCacheView& kc, bool split = false);
-// R of items [r0, r0 + rcnt) of an n-item batch, and the distinct keys when `keys`
-void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, bool keys, const uint8_t* sig,
+                       const KeyCacheView& kc, bool split = false, uint32_t klanes = 0);
+// R of items [r0, r0 + rcnt) of an n-item batch, and the distinct keys on klanes lanes (0: none;
+// launch_decompress: 0 = n, one lane per possible key)
+void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, uint32_t klanes, const uint8_t* sig,
                              const uint8_t* vk, const uint32_t* key_rep, bool per_sig, uint32_t* pts, uint8_t* itembad,
                              uint8_t* keybad, int* flags, const KeyCacheView& kc, bool split = false);
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,

@@ -216,9 +216,11 @@ __device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
 }
 
 // n: the batch's items (key points sit at 1 + n + j); this launch decodes R of items
-// [r0, r0 + rcnt) and, with `keys`, the distinct keys (a chunked host-buffer call decodes each
-// chunk's R as it lands and the keys once the key grouping is done).
-__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, uint32_t rcnt, int keys,
+// [r0, r0 + rcnt) and, on `klanes` key lanes (0: none), the distinct keys (a chunked host-buffer
+// call decodes each chunk's R as it lands and the keys once the key grouping is done). The key
+// count m is only known on the device: the host sizes klanes from the previous grouped batch, and
+// a lane decodes keys j, j + klanes, ... when m is larger.
+__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, uint32_t rcnt, uint32_t klanes,
                                                        const uint8_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep, int per_sig_host,
@@ -238,12 +240,10 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, 
     return;
   }
   const uint32_t kbase = (rcnt + 63u) & ~63u;   // key lanes start on a wave boundary (no R/key divergence)
-  if (!keys || lane < kbase) return;
-  const uint32_t i = lane;
-  const uint32_t j = i - kbase;
+  if (lane < kbase || lane - kbase >= klanes) return;
   const uint32_t m = (uint32_t)flags[FLAG_NKEYS];
-  if (j >= m) return;
   const bool per_sig = per_sig_host || flags[FLAG_OVF];
+  for (uint32_t j = lane - kbase; j < m; j += klanes) {
   ld_words8(vk + (size_t)(per_sig ? j : key_rep[j]) * 32, w);
   const int ci = kc_lookup(kcache, w);
   bool ok;
@@ -262,6 +262,7 @@ __global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, 
   if (split && j == 0) copy_record(pts, split_b_hi_point(n, m), kcache.bcomb + (size_t)COMB_SHIFT128 * NIELS_WORDS);
   keybad[j] = ok ? 0 : 1;
   if (!ok) atomicOr(&flags[FLAG_BAD], 1);
+  }
 }
 
 // Slot hash of the raw key bytes under a 64-bit per-context secret (drawn from OS randomness
@@ -753,23 +754,25 @@ void launch_challenge(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8
   if (n)
     hipLaunchKernelGGL(k_challenge, dim3(cdiv(n, SHA_THREADS)), dim3(SHA_THREADS), 0, st, n, vk, sig, msg, off, k);
 }
-void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, bool keys, const uint8_t* sig,
+void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t rcnt, uint32_t klanes, const uint8_t* sig,
                              const uint8_t* vk, const uint32_t* key_rep, bool per_sig, uint32_t* pts, uint8_t* itembad,
                              uint8_t* keybad, int* flags, const KeyCacheView& kc, bool split) {
-  // lanes [0, rcnt) decode R; the key lanes start at the next wave boundary and cover the largest
-  // possible key count (m <= n). A wave holding both would run both decodes one after the other,
-  // which doubles a small batch's decode latency. Small launches use one wave per workgroup so
-  // that the waves spread over CUs instead of sharing SIMDs.
-  const uint64_t lanes = ((rcnt + 63ull) & ~63ull) + (keys ? n : 0u);
+  // lanes [0, rcnt) decode R; the key lanes start at the next wave boundary. A wave holding both
+  // would run both decodes one after the other, which doubles a small batch's decode latency.
+  // Small launches use one wave per workgroup so that the waves spread over CUs instead of sharing
+  // SIMDs.
+  if (klanes > n) klanes = n;
+  const uint64_t lanes = ((rcnt + 63ull) & ~63ull) + klanes;
   if (!n || !lanes) return;
   const uint32_t block = lanes <= 16384 ? 64 : 256;
-  hipLaunchKernelGGL(k_decompress, dim3(cdiv(lanes, block)), dim3(block), 0, st, n, r0, rcnt, keys ? 1 : 0, sig, vk,
+  hipLaunchKernelGGL(k_decompress, dim3(cdiv(lanes, block)), dim3(block), 0, st, n, r0, rcnt, klanes, sig, vk,
                      key_rep, per_sig ? 1 : 0, pts, itembad, keybad, flags, kc, split ? 1 : 0);
 }
 void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uint8_t* vk, const uint32_t* key_rep,
                        bool per_sig, uint32_t* pts, uint8_t* itembad, uint8_t* keybad, int* flags,
-                       const KeyCacheView& kc, bool split) {
-  launch_decompress_range(st, n, 0, n, true, sig, vk, key_rep, per_sig, pts, itembad, keybad, flags, kc, split);
+                       const KeyCacheView& kc, bool split, uint32_t klanes) {
+  launch_decompress_range(st, n, 0, n, klanes ? klanes : n, sig, vk, key_rep, per_sig, pts, itembad, keybad, flags, kc,
+                          split);
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
