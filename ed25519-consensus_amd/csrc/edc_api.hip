@@ -337,7 +337,8 @@ static int ensure_msm(edc_ctx* ctx, Slot& s, const MsmPlan& P, size_t entries) {
     s.cap_entries = 0;
     const size_t cap = entries + entries / 8 + 1024;
     CK(dalloc(&s.entries, cap));
-    CK(dalloc(&s.sorted, cap));
+    // + 256 per possible bin: each bin's lane-major region is padded to whole rounds (k_msm_sort)
+    CK(dalloc(&s.sorted, cap + 256 * (size_t)MSM_MAX_BINS));
     s.cap_entries = cap;
   }
   return 0;

@@ -364,11 +364,39 @@ __device__ __forceinline__ uint32_t* bucket_slot(uint32_t* buckets, uint32_t bin
   return buckets + ((size_t)bin * NSLICE + b) * EXT_WORDS;
 }
 
-// Counting sort of each bin's entries by bucket (one workgroup per bin): sorted[] gets the point
-// indices (sign in bit 31) bucket by bucket, bucket_end[] the exclusive end position of every
-// bucket, and empty buckets get the identity. A kernel of its own, so the memory-bound sort of one
+// Counting sort of each bin's entries by bucket (one workgroup per bin): the point indices (sign in
+// bit 31) go out bucket by bucket, bucket_end[] gets the exclusive end position of every bucket,
+// and empty buckets get the identity. The accumulation's lane t walks the sorted positions
+// [lo_t, hi_t) = [E t / 256, E (t+1) / 256) one per round, so position q is stored LANE-MAJOR at
+// sorted_slot(bin, q) = offsets[bin] + 256 bin + 256 j + t (t its lane, j = q - lo_t its round): a
+// round's 64 lanes then read one contiguous 256-byte run of `sorted` instead of 64 words on 64
+// lines (each lane re-reading its own line every round, which the row gathers evicted from L2
+// in between). Each bin's region is padded to 256 x rounds slots: 256 more per bin in total. A kernel of its own, so the memory-bound sort of one
 // batch overlaps the VALU-bound accumulation of another instead of idling the accumulation's CUs
 // (every workgroup of a launch sorts at the same time).
+// lane of the accumulation that owns sorted position q of a bin of E entries (lo_t <= q < hi_t
+// with lo_t = (E t) >> 8): the largest t with lo_t <= q, which is floor((256 q + 255) / E) -- with
+// E < 256 several lanes share one lo and only the last of them owns it. A float estimate of that
+// quotient is within one of it; one exact step fixes it.
+__device__ __forceinline__ uint32_t acc_lane_of(uint32_t q, uint32_t E, float invE) {
+  uint32_t t = (uint32_t)(((float)q * 256.0f + 255.0f) * invE);
+  t = t > 255u ? 255u : t;
+  if ((uint32_t)(((uint64_t)E * t) >> 8) > q) --t;
+  else if (t < 255u && (uint32_t)(((uint64_t)E * (t + 1)) >> 8) <= q) ++t;
+  return t;
+}
+#ifndef EDC_SORT_LANE_MAJOR
+#define EDC_SORT_LANE_MAJOR 1   // measurement knob: 0 = the round-5 position-major layout (A/B builds)
+#endif
+__device__ __forceinline__ uint32_t sorted_slot(uint32_t base, uint32_t q, uint32_t E, float invE) {
+#if EDC_SORT_LANE_MAJOR
+  const uint32_t t = acc_lane_of(q, E, invE);
+  return base + 256u * (q - (uint32_t)(((uint64_t)E * t) >> 8)) + t;
+#else
+  return base + q;
+#endif
+}
+
 #ifndef EDC_SORT_REG
 #define EDC_SORT_REG 40
 #endif
@@ -384,6 +412,8 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
   const uint32_t E = counts[bin];
   if (E == 0) return;
   const uint32_t off = offsets[bin];
+  const uint32_t tbase = off + 256u * bin;            // the bin's lane-major region
+  const float invE = 1.0f / (float)E;
   lcnt[t] = 0;
   __syncthreads();
   // the first SORT_REG * 256 entries are read once and kept in registers for the second pass
@@ -424,14 +454,14 @@ __global__ void __launch_bounds__(256) k_msm_sort(const uint32_t* __restrict__ c
   if (lcnt[t] == 0) st_ext(bucket_slot(buckets, bin, t), ge_identity());
 #pragma unroll
   for (int u = 0; u < SORT_REG; ++u)
-    if (reg[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[reg[u].y], 1u)] = reg[u].x;
+    if (reg[u].y != 0xFFFFFFFFu) sorted[sorted_slot(tbase, atomicAdd(&lcur[reg[u].y], 1u), E, invE)] = reg[u].x;
   for (uint32_t e0 = t + 256u * SORT_REG; e0 < E; e0 += 256 * SB) {
     uint2 en[SB];
 #pragma unroll
     for (int u = 0; u < SB; ++u) en[u] = e0 + 256u * u < E ? entries[off + e0 + 256u * u] : make_uint2(0u, 0xFFFFFFFFu);
 #pragma unroll
     for (int u = 0; u < SB; ++u)
-      if (en[u].y != 0xFFFFFFFFu) sorted[off + atomicAdd(&lcur[en[u].y], 1u)] = en[u].x;
+      if (en[u].y != 0xFFFFFFFFu) sorted[sorted_slot(tbase, atomicAdd(&lcur[en[u].y], 1u), E, invE)] = en[u].x;
   }
 }
 
@@ -512,8 +542,16 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
     }
   };
   // software pipeline: the rows of round j + 1 are in flight while round j's addition runs
-  uint32_t e = lo < hi ? sorted[off + lo] : 0u;
-  uint32_t e_next = lo + 1 < hi ? sorted[off + lo + 1] : e;
+  // this lane's positions, lane-major (k_msm_sort): round j's index at srow[256 j]
+#if EDC_SORT_LANE_MAJOR
+  const uint32_t* srow = sorted + off + 256u * bin + t;
+  constexpr uint32_t SSTEP = 256;
+#else
+  const uint32_t* srow = sorted + off + 256u * bin + lo;
+  constexpr uint32_t SSTEP = 1;
+#endif
+  uint32_t e = lo < hi ? srow[0] : 0u;
+  uint32_t e_next = lo + 1 < hi ? srow[SSTEP] : e;
   gather_rows(e & 0x7FFFFFFFu);
 #if EDC_ACC_PROBE >= 2
   __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -540,7 +578,7 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
 #endif
     const uint32_t e_cur = e;
     e = e_next;
-    if (pos + 2 < hi) e_next = sorted[off + pos + 2];
+    if (pos + 2 < hi) e_next = srow[SSTEP * (j + 2)];
     if (pos < hi) {
       acc = ge_madd_sgn(acc, q, (e_cur >> 31) != 0);
     }

@@ -91,6 +91,13 @@ for step in "$@"; do
         python3 tools/rocpd_stats.py "gpurun_out/${tag}_$p/k_results.db" > "gpurun_out/${tag}_${p}_kernel_stats.csv" || exit 1
       done ;;
     pmc) run pmc 600 bash tools/pmc_passes.sh ;;
+    # FETCH_SIZE / WRITE_SIZE passes of one build (base = libedc.so), one batch at a time:
+    # gpurun_out/<tag>_pmcf_<v>_{fetch,write}/ for tools/pmc_batch_table.py-style summaries
+    pmcf=*)
+      v=${step#pmcf=}; lib=$PWD/$D/libedc_$v.so; [ "$v" = base ] && lib=$PWD/$D/libedc.so
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run pmcf_${v}_$c 150 env EDC_SINGLE_STREAM=1 timeout -s KILL 120 rocprofv3 --pmc $c -d gpurun_out/${tag}_pmcf_${v}_$c -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --no-host-api --profile-steps 1 --lib "$lib"
+      done ;;
     rccl1) run rccl1 300 env EDC_FORCE_DIST=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
     gloo2)
       run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
