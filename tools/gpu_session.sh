@@ -84,8 +84,8 @@ for step in "$@"; do
     small) run small 300 python3 -u tools/smallbatch_bench.py ;;
     multi) run multi 300 python3 -u tools/multi_bench.py ;;
     prof)
-      run prof1 300 env EDC_SINGLE_STREAM=1 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline
-      run profp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profp -o k -- python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline
+      run prof1 300 env EDC_SINGLE_STREAM=1 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof1 -o k -- python3 -u bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-host-api
+      run profp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_profp -o k -- python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-api
       # --stats layout from the trace database (this image's rocprofv3 writes rocpd databases)
       for p in prof1 profp; do
         python3 tools/rocpd_stats.py "gpurun_out/${tag}_$p/k_results.db" > "gpurun_out/${tag}_${p}_kernel_stats.csv" || exit 1

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --profile-steps 1 $BENCH_ARGS > gpurun_out/pmc_$name.log 2>&1
+    python3 bench.py --steps 2 --warmup 1 --inflight 1 --no-cpu-baseline --no-host-api --profile-steps 1 $BENCH_ARGS > gpurun_out/pmc_$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"; return $rc
 }
 run valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE &&
