@@ -184,8 +184,8 @@ struct edc_ctx {
   uint64_t mu_hits = 0, mu_reruns = 0;  // union-first launches that passed / were rerun per batch
   // chunked synchronous host-buffer calls (run_host_chunked): a copy stream and one event per
   // chunk (+ the keys / offsets piece), created on first use
-  hipStream_t hcs = nullptr;
-  hipEvent_t hev[9] = {};
+  hipStream_t hcs = nullptr, hcs2 = nullptr;
+  hipEvent_t hev[9] = {}, hev2[9] = {};   // piece 0 + signature chunks / k or message chunks
   hipStream_t st() const { return slot[0].st; }
   KeyCacheView kc() const {
     if (!kc_m) return KeyCacheView{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr, 0, 0};
@@ -1103,7 +1103,9 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
   if (rc) return rc;
   if (!ctx->hcs) {
     CK(hipStreamCreateWithFlags(&ctx->hcs, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&ctx->hcs2, hipStreamNonBlocking));
     for (hipEvent_t& e : ctx->hev) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : ctx->hev2) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   const bool per_sig = choose_per_sig(ctx, n), split = choose_split(ctx);
   const MsmPlan P = batch_plan(ctx, n, per_sig, split);
@@ -1129,8 +1131,12 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
   const uint64_t salt64 = per_sig ? 0 : splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
   const KeyCacheView kc = ctx->kc();
 
-  // the launcher thread: every kernel, each piece's behind that piece's event
-  HostGate gate;
+  // the launcher thread: every kernel, each piece's behind that piece's events. Two copying
+  // threads: this one (keys / offsets / z, then the signature chunks) and a second one (the k or
+  // message chunks) on its own stream, so that one thread's per-copy host work (~20-25 us per
+  // pageable copy before its transfer starts) runs while the other's transfer is on the bus
+  static const bool one_copier = getenv("EDC_HOST_COPY_THREADS") && getenv("EDC_HOST_COPY_THREADS")[0] == '1';
+  HostGate gate, gate2;
   std::string lerr;
   int lrc = 0;
   std::thread launcher([&] {
@@ -1166,6 +1172,10 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
       launch_decompress_range(st2, N, (uint32_t)c0, (uint32_t)cnt, 0, ctx->sig, ctx->vk, s.key_rep, per_sig, s.pts,
                               s.itembad + s.cap_n, s.keybad, s.flags, kc, split);
       LK(hipStreamWaitEvent(st, ev, 0));
+      if (!one_copier) {
+        if (!gate2.wait(c + 1)) return;
+        LK(hipStreamWaitEvent(st, ctx->hev2[c], 0));
+      }
       if (!k)
         launch_challenge(st, (uint32_t)cnt, ctx->vk + c0 * 32, ctx->sig + c0 * 64, ctx->msg, ctx->off + c0,
                          s.k + c0 * 8);
@@ -1185,6 +1195,35 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
 #undef LK
   });
 
+  // the k / message chunks (second copying thread, or this one after each signature chunk)
+  auto copy_second = [&](int c, hipStream_t str, hipEvent_t ev, std::string& err) -> int {
+    const size_t c0 = cb[c], cnt = cb[c + 1] - cb[c];
+    hipError_t e = hipSuccess;
+    if (k) {
+      e = hipMemcpyAsync(s.k + c0 * 8, k + c0 * 32, cnt * 32, hipMemcpyHostToDevice, str);
+    } else {
+      const size_t b0 = (size_t)(msg_off[c0] - msg_off[0]), b1 = (size_t)(msg_off[c0 + cnt] - msg_off[0]);
+      if (b1 > b0) e = hipMemcpyAsync(ctx->msg + b0, msg + msg_off[c0], b1 - b0, hipMemcpyHostToDevice, str);
+    }
+    if (e == hipSuccess && ev) e = hipEventRecord(ev, str);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      err = std::string("host chunk copy: ") + hipGetErrorString(e);
+      return EDC_ERR_HIP;
+    }
+    return 0;
+  };
+  std::string err2;
+  int rc2 = 0;
+  std::thread copier2;
+  if (!one_copier)
+    copier2 = std::thread([&] {
+      if (hipSetDevice(ctx->device) != hipSuccess) { rc2 = EDC_ERR_HIP; gate2.stop(); return; }
+      for (int c = 0; c < nchunks; ++c) {
+        if ((rc2 = copy_second(c, ctx->hcs2, ctx->hev2[c], err2))) { gate2.stop(); return; }
+        gate2.post(c + 1);
+      }
+    });
   // this thread: the copies, back to back, one event per piece
   auto copies = [&]() -> int {
     CK(hipMemcpyAsync(ctx->vk, vk, n * 32, hipMemcpyHostToDevice, cs));
@@ -1197,11 +1236,9 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
     for (int c = 0; c < nchunks; ++c) {
       const size_t c0 = cb[c], cnt = cb[c + 1] - cb[c];
       CK(hipMemcpyAsync(ctx->sig + c0 * 64, sig + c0 * 64, cnt * 64, hipMemcpyHostToDevice, cs));
-      if (k) {
-        CK(hipMemcpyAsync(s.k + c0 * 8, k + c0 * 32, cnt * 32, hipMemcpyHostToDevice, cs));
-      } else {
-        const size_t b0 = (size_t)(msg_off[c0] - msg_off[0]), b1 = (size_t)(msg_off[c0 + cnt] - msg_off[0]);
-        if (b1 > b0) CK(hipMemcpyAsync(ctx->msg + b0, msg + msg_off[c0], b1 - b0, hipMemcpyHostToDevice, cs));
+      if (one_copier) {
+        std::string e1;
+        if (int r = copy_second(c, cs, nullptr, e1)) { ctx->err = e1; return r; }
       }
       CK(hipEventRecord(ctx->hev[c + 1], cs));
       gate.post(c + 2);
@@ -1209,9 +1246,12 @@ static int enqueue_host_chunked(edc_ctx* ctx, size_t n, const uint8_t* vk, const
     return 0;
   };
   rc = copies();
-  if (rc) gate.stop();
+  if (rc) { gate.stop(); gate2.stop(); }
+  if (copier2.joinable()) copier2.join();
+  if (rc2) gate.stop();
   launcher.join();
   if (rc) return rc;
+  if (rc2) { ctx->err = err2; return rc2; }
   if (lrc) { ctx->err = lerr; return lrc; }
   s.acc_nbin = P.nbin();
   s.pending = true;
@@ -1248,6 +1288,7 @@ static int run_host_sync(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_
   const int rc = enqueue_host_chunked(ctx, n, vk, sig, msg, msg_off, k, z, z_seed, check8 != nullptr, rebased);
   if (rc) {     // nothing may still read the staging buffers or the caller's memory
     (void)hipStreamSynchronize(ctx->hcs);
+    (void)hipStreamSynchronize(ctx->hcs2);
     (void)hipStreamSynchronize(s.st2);
     (void)hipStreamSynchronize(s.st);
     s.pending = false;
@@ -1354,9 +1395,13 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.st) (void)hipStreamDestroy(s.st);
   }
   if (ctx->hcs) (void)hipStreamSynchronize(ctx->hcs);
+  if (ctx->hcs2) (void)hipStreamSynchronize(ctx->hcs2);
   for (hipEvent_t e : ctx->hev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->hev2)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->hcs) (void)hipStreamDestroy(ctx->hcs);
+  if (ctx->hcs2) (void)hipStreamDestroy(ctx->hcs2);
   void* ptrs[] = {ctx->vk, ctx->sig, ctx->msg, ctx->zexp, ctx->off, ctx->kbuf, ctx->verdicts, ctx->vtab, ctx->aux,
                   ctx->btab, ctx->comb_in, ctx->fb_xpt, ctx->fb_xrg, ctx->fb_xscal, ctx->fb_rv, ctx->fb_idx,
                   ctx->fb_g};
