@@ -220,7 +220,10 @@ __device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
 // call decodes each chunk's R as it lands and the keys once the key grouping is done). The key
 // count m is only known on the device: the host sizes klanes from the previous grouped batch, and
 // a lane decodes keys j, j + klanes, ... when m is larger.
-__global__ void __launch_bounds__(256, 4) k_decompress(uint32_t n, uint32_t r0, uint32_t rcnt, uint32_t klanes,
+#ifndef EDC_DEC_OCC
+#define EDC_DEC_OCC 4   // waves per SIMD the decode is compiled for (128 VGPRs; 5 -> 96 with spills outside the squaring loops)
+#endif
+__global__ void __launch_bounds__(256, EDC_DEC_OCC) k_decompress(uint32_t n, uint32_t r0, uint32_t rcnt, uint32_t klanes,
                                                        const uint8_t* __restrict__ sig,
                                                        const uint8_t* __restrict__ vk,
                                                        const uint32_t* __restrict__ key_rep, int per_sig_host,
