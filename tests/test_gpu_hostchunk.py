@@ -9,7 +9,10 @@ context plans dense/grouped, the second adaptively: few-keys windows, per-signat
 Cases: vote batches (150 validators) and distinct keys; ragged n (a partial last chunk) and n at
 the 2^16 threshold; 0..1024-byte messages with offsets that do not start at 0; a wrong signature in
 the last chunk (a non-identity check8); an undecodable R in the last chunk and an s = l in the first
-(the bad flag: code 1, zero check8); caller-drawn z."""
+(the bad flag: code 1, zero check8); caller-drawn z. Grouped batches accumulate each chunk's R
+terms into the MSM buckets as the chunk lands and add the key / B terms at the end; key grouping
+forced for distinct keys (70,001 key terms at the end) and the device's grouping overflow (one A_i
+term per signature at the end, FLAG_OVF) are covered too."""
 import ctypes
 import os
 import sys
@@ -65,21 +68,25 @@ def _host_copies(vk, sig, msg, off, n, shift):
     return hv, hs, hm, (ctypes.c_uint64 * (n + 1)).from_buffer_copy(o.tobytes())
 
 
-CASES = [   # (n, validators (0 = distinct), message bytes (-1 = 0..1024), corruption)
-    (70001, 150, 120, "wrong_sig"),
-    (65536, 0, 32, "wrong_sig"),
-    (70001, 0, -1, "wrong_sig"),
-    (98304 + 77, 150, 120, "bad_r_and_s"),
-    (70001, 150, 120, "none"),
-    (1 << 20, 150, 120, "wrong_sig"),
+CASES = [   # (n, validators (0 = distinct), message bytes (-1 = 0..1024), corruption, key grouping mode)
+    (70001, 150, 120, "wrong_sig", 0),
+    (65536, 0, 32, "wrong_sig", 0),
+    (70001, 0, -1, "wrong_sig", 0),
+    (98304 + 77, 150, 120, "bad_r_and_s", 0),
+    (70001, 150, 120, "none", 0),
+    (1 << 20, 150, 120, "wrong_sig", 0),
+    (70001, 0, 32, "none", 1),          # always grouped: every distinct key a term at the end
+    (70001, 150, 120, "wrong_sig", 3),  # grouping overflow on the device: per-signature A_i terms
+    (70001, 150, 120, "none", 3),
 ]
 
 
-@pytest.mark.parametrize("n,keys,mlen,kind", CASES, ids=lambda v: str(v))
-def test_host_chunked_equals_device(env, n, keys, mlen, kind):
+@pytest.mark.parametrize("n,keys,mlen,kind,grouping", CASES, ids=lambda v: str(v))
+def test_host_chunked_equals_device(env, n, keys, mlen, kind, grouping):
     torch, bench, edc = env
     eng = edc.Engine(0)
     try:
+        eng.set_key_grouping(grouping)
         vk, sig, msg, off = _workload(env, eng, n, keys, mlen)
         _corrupt(kind, vk, sig, msg, off, n)
         hv, hs, hm, ho = _host_copies(vk, sig, msg, off, n, shift=5)

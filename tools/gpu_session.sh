@@ -27,6 +27,8 @@
 #   pre              configs[2] with prehashed items (edc_batch_submit_prehashed_device)
 #   m17 | m16        8 consecutive 2^17 vote shards / configs[1] batches per launch (--multi 8, union first)
 #   m17x | m16x      the same batch by batch (--multi-exact)
+#   hapi | hapi0     the host_api leg: chunked (default) / one piece
+#   htrace           rocprofv3 copy + kernel trace of synchronous host-buffer calls, last call's timeline
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -127,6 +129,11 @@ for step in "$@"; do
           python3 -c "import json,sys; d=json.loads(open('$(log hapi_$v)').read().strip().splitlines()[-1]); print('hapi=$v', json.dumps(d['host_api']))" | tee -a "gpurun_out/${tag}_summary.log" ;;
     hapi0) run hapi0 300 env EDC_HOST_CHUNKS=0 python3 -u bench.py --steps 10 --warmup 3 --no-cpu-baseline
           python3 -c "import json,sys; d=json.loads(open('$(log hapi0)').read().strip().splitlines()[-1]); print('hapi0', json.dumps(d['host_api']))" | tee -a "gpurun_out/${tag}_summary.log" ;;
+    # copies and kernels of one synchronous host-buffer call on one time axis (tools/host_timeline.py)
+    htrace)
+      run htrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/${tag}_htrace -o ht -- python3 -u tools/host_trace.py
+      python3 tools/host_timeline.py gpurun_out/${tag}_htrace > "gpurun_out/${tag}_htrace_timeline.txt" || exit 1
+      head -1 "gpurun_out/${tag}_htrace_timeline.txt" ;;
     ab=*)
       IFS=, read -ra libs <<< "${step#ab=}"
       for rep in $(seq 1 "${AB_REPS:-2}"); do
