@@ -1038,7 +1038,10 @@ static inline uint32_t cdiv(uint64_t a, uint32_t b) { return (uint32_t)((a + b -
 static constexpr size_t kScatterLdsMax = 160 * 1024 - 256;   // k_msm_scatter's dynamic LDS ceiling
 // entries of the scatter's LDS stage (process-wide; edc_debug_set_scatter_stage lowers it so that
 // tests can drive the direct-store path, which the default stage covers only at large bin counts)
-static uint32_t g_scatter_stage_max = 16384;
+#ifndef EDC_SCATTER_STAGE
+#define EDC_SCATTER_STAGE 16384   // measurement knob (A/B builds); the debug entry lowers it at run time
+#endif
+static uint32_t g_scatter_stage_max = EDC_SCATTER_STAGE;
 extern "C" int edc_debug_set_scatter_stage(uint32_t max_entries) {
   g_scatter_stage_max = max_entries > 16384 ? 16384u : max_entries;
   return 0;
