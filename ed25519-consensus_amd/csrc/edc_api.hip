@@ -351,7 +351,7 @@ static int ensure_msm(edc_ctx* ctx, Slot& s, const MsmPlan& P, size_t entries) {
 // each, so no window-combine pass runs before the Horner pass (~90 us of latency per call).
 static int auto_window_bits(size_t n) {
   if (n >= (1u << 19)) return 16;
-  if (n >= (1u << 17)) return 15;   // 9 z windows; 14 bits (10 windows) measured 2 % slower at 2^17 with 16 in flight
+  if (n >= (1u << 17)) return 15;   // 9 z windows; 14 bits 2 % and 16 bits 15 % slower at 2^17 (r06w)
   if (n >= (1u << 15)) return 13;
   if (n >= (1u << 13)) return 12;
   return 9;
