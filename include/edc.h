@@ -64,6 +64,10 @@ const char* edc_last_error(const edc_ctx* ctx);
  * undecodable A/R or non-canonical s, as the reference). check8 (nullable) receives the
  * compressed [8]*check point when the equation was evaluated (zeros when the batch was
  * rejected before the MSM).
+ * Host-buffer synchronous calls (this one, edc_batch_verify_z, edc_batch_verify_prehashed) from
+ * 2^16 items copy their inputs in chunks and start each chunk's work as it lands; for the call's
+ * duration the engine runs two helper threads of its own on ctx (joined before it returns), so
+ * the one-context-per-thread rule below is unchanged. Results equal the one-piece path's.
  */
 int edc_batch_verify(edc_ctx* ctx, size_t n, const uint8_t* vk, const uint8_t* sig,
                      const uint8_t* msg, const uint64_t* msg_off, const uint8_t z_seed[32],
