@@ -102,7 +102,7 @@ for step in "$@"; do
       done ;;
     rccl1) run rccl1 300 env EDC_FORCE_DIST=1 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --steps 40 --warmup 5 --no-cpu-baseline ;;
     gloo2)
-      run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline
+      run gloo2_weak 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --scaling weak --steps 20 --warmup 3 --no-cpu-baseline
       run gloo2_strong 300 env EDC_DIST_BACKEND=gloo python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --scaling strong --steps 20 --warmup 3 --no-cpu-baseline ;;
     lat) run lat 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 ;;
     lat=*) v=${step#lat=}; run lat_$v 300 python3 -u tools/latency_probe.py --sizes c3,n17,c2,n150 --lib "$PWD/$D/libedc_$v.so" ;;
