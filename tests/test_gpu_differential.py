@@ -6,7 +6,8 @@ corrupted signatures and messages, s >= l, undecodable R and A encodings (tests/
 and duplicated items. For every batch the GPU's verdict and [8]*check (src/batch.rs:149-217) and
 every item's verify_single code (src/batch.rs:104-107, verification_key.rs:225-258) must equal the
 oracle's, through the message path, the prehashed path and (for sizes that allow it) a union-first
-multi launch of the batch split in two."""
+multi launch of the batch split in two. EDC_DIFF_SEEDS=<k> runs k seeds of each test instead of the
+default 8 / 3 (soak runs of the final tree: profiles/r06/r06z_differential_soak.log)."""
 import os
 import random
 import sys
@@ -68,7 +69,10 @@ def _batch(engine, rnd, n, hard=None):
     return vks, sigs, msgs
 
 
-@pytest.mark.parametrize("seed", range(8))
+SOAK = int(os.environ.get("EDC_DIFF_SEEDS", "0"))
+
+
+@pytest.mark.parametrize("seed", range(SOAK or 8))
 def test_mixed_batches_vs_oracle(engine, oc, seed):
     rnd = random.Random(9000 + seed)
     codes = []
@@ -91,10 +95,11 @@ def test_mixed_batches_vs_oracle(engine, oc, seed):
             assert engine.verify_each(vks, sigs, msgs) == exp_each, tag
             assert engine.verify_prehashed_each(vks, sigs, ks) == exp_each, tag
     print(f"\n[differential] seed {seed}: (n, code, evaluated) {codes}")
-    assert any(c == 0 for _, c, _ in codes) and any(c == 1 for _, c, _ in codes)
+    if not SOAK:   # the fixed seeds draw both outcomes; a soak seed may draw only failing batches
+        assert any(c == 0 for _, c, _ in codes) and any(c == 1 for _, c, _ in codes)
 
 
-@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("seed", range(SOAK or 3))
 def test_mixed_multi_union_vs_oracle(engine, oc, seed):
     """The same mixtures as two consecutive batches of one union-first launch: each batch's
     verdict and check8 equal the oracle's for that batch at its global z offset."""
