@@ -8,7 +8,10 @@ parts (summed per window); 8-bit high windows for the B / key
 coefficients (chosen when the previous grouped batch on the context had few distinct keys) and
 full-width windows otherwise; grouped keys, one key term per signature, and the on-device overflow
 path of key grouping (set_key_grouping(3): grouping abandoned mid-batch, as adversarial keys would
-cause). Each batch is verified twice, so the second run uses the plan hinted by the first."""
+cause). Each batch is verified twice, so the second run uses the plan hinted by the first.
+Randomized shapes (test_random_plans_match_oracle): n, key count, window width, parts, message
+length and the bad item drawn per case, 6 cases by default, EDC_PLAN_SOAK=<k> for a soak run."""
+import os
 import random
 
 import pytest
@@ -87,3 +90,28 @@ def test_scatter_direct_path_matches_oracle(engine, oracle_c, stage, n, m, bad, 
     finally:
         engine.set_msm_shape(0, 0)
         engine.lib.edc_debug_set_scatter_stage(16384)
+
+
+PLAN_SOAK = int(os.environ.get("EDC_PLAN_SOAK", "0"))
+
+
+@pytest.mark.parametrize("case", range(PLAN_SOAK or 6))
+def test_random_plans_match_oracle(engine, oracle_c, case):
+    """bins from a few entries (E < 256: several accumulation lanes share a start, the lane-major
+    index mapping's edge) to thousands, any window width the API accepts and 0..16 parts"""
+    rnd = random.Random(31337 + case)
+    n = rnd.choice([rnd.randrange(1, 300), rnd.randrange(300, 5000), rnd.randrange(5000, 20000)])
+    m = rnd.choice([1, rnd.randrange(1, 200), max(1, n // rnd.choice([1, 2, 7, 50]))])
+    bits = rnd.choice([0, 9, 10, 11, 12, 13, 14, 15, 16])
+    parts = rnd.choice([0, 1, 2, 3, 4, 8, 16])
+    bad = rnd.choice([None, rnd.randrange(n)])
+    vks, sigs, msgs, zseed = _batch(engine, n, m, bad, msg_len=rnd.randrange(0 if bad is None else 1, 300),
+                                        seed=case)
+    exp_code, exp_c8 = oracle_c.batch_verify(list(zip(vks, sigs, msgs)), zseed)
+    engine.set_msm_shape(bits, parts)
+    try:
+        for _ in range(2):
+            got = engine.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True)
+            assert got == (exp_code, exp_c8), (case, n, m, bits, parts, bad)
+    finally:
+        engine.set_msm_shape(0, 0)
