@@ -73,7 +73,10 @@ def make_workload(pkg, eng, torch, dev, n, keys, msg_len, global_base):
         assert global_base % 2 == 0
         seeds = chacha_device(pkg, eng, torch, bytes([0x11]) * 32, global_base // 2, (n + 1) // 2, dev)[: n * 32]
         idx = torch.arange(0, n, dtype=torch.int32, device=dev)
-    if msg_len >= 0:
+    if msg_len == 0:                                 # empty messages (the reference benches/bench.rs shape)
+        msg = torch.zeros(1, dtype=torch.uint8, device=dev)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    elif msg_len > 0:
         stride = (msg_len + 63) // 64 * 64
         blocks_per_msg = stride // 64
         raw = chacha_device(pkg, eng, torch, bytes([0x22]) * 32, global_base * blocks_per_msg, n * blocks_per_msg, dev)

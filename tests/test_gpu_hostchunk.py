@@ -134,3 +134,49 @@ def test_host_chunked_small_and_empty(engine):
     c8 = ctypes.create_string_buffer(32)
     assert lib.edc_batch_verify_prehashed(engine.ctx, 0, b"\0", b"\0", b"\0", bytes(32), None, c8) == 0
     assert c8.raw == bytes([1]) + bytes(31)
+
+
+HOST_SOAK = int(os.environ.get("EDC_HOSTCHUNK_SOAK", "0"))
+
+
+@pytest.mark.parametrize("case", range(HOST_SOAK or 3))
+def test_random_host_chunked_equals_device(env, case):
+    """random n (chunk counts 1..7 plus the last chunk, ragged edges), validators or distinct keys,
+    message lengths, corruption and key-grouping mode; EDC_HOSTCHUNK_SOAK=<k> for a soak run"""
+    import random
+    torch, bench, edc = env
+    rnd = random.Random(4242 + case)
+    n = rnd.randrange(1 << 16, 1 << 21 if case % 4 == 3 else 1 << 19)
+    keys = rnd.choice([150, 0, rnd.randrange(1, 5000)])
+    mlen = rnd.choice([-1, 0, 32, 120, rnd.randrange(1, 400)])
+    kind = rnd.choice(["none", "wrong_sig", "bad_r_and_s"])
+    grouping = rnd.choice([0, 0, 1, 3])
+    eng = edc.Engine(0)
+    try:
+        eng.set_key_grouping(grouping)
+        vk, sig, msg, off = _workload(env, eng, n, keys, mlen)
+        if kind == "wrong_sig" and mlen == 0:
+            kind = "bad_r_and_s"
+        _corrupt(kind, vk, sig, msg, off, n)
+        hv, hs, hm, ho = _host_copies(vk, sig, msg, off, n, shift=rnd.randrange(0, 40))
+        lib = eng.lib
+        zseed = rnd.randbytes(32)
+        kb = ctypes.create_string_buffer(32 * n)
+        eng._check(lib.edc_challenge(eng.ctx, n, hv, hs, hm, ho, kb))
+        d_k = torch.frombuffer(bytearray(kb.raw), dtype=torch.uint8).to("cuda:0")
+        torch.cuda.synchronize()
+        want = 0 if kind == "none" else 1
+        tag = (case, n, keys, mlen, kind, grouping)
+        for rep in range(2):
+            c_dev, c_host = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+            r_dev = lib.edc_batch_verify_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), msg.data_ptr(),
+                                                off.data_ptr(), zseed, 0, None, c_dev)
+            r_host = lib.edc_batch_verify(eng.ctx, n, hv, hs, hm, ho, zseed, c_host)
+            assert (r_host, c_host.raw) == (r_dev, c_dev.raw) and r_dev == want, (tag, rep, "messages")
+            c_dev, c_host = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32)
+            r_dev = lib.edc_batch_verify_prehashed_device(eng.ctx, n, vk.data_ptr(), sig.data_ptr(), d_k.data_ptr(),
+                                                          zseed, 0, None, c_dev)
+            r_host = lib.edc_batch_verify_prehashed(eng.ctx, n, hv, hs, kb.raw, zseed, None, c_host)
+            assert (r_host, c_host.raw) == (r_dev, c_dev.raw) and r_dev == want, (tag, rep, "prehashed")
+    finally:
+        eng.close()
