@@ -4,7 +4,9 @@ lo + 2^128 hi on the point and on its cached [2^128] multiple; the MSM (src/batc
 same group element, so the verdict and the compressed [8]*check must equal the unsplit evaluation's
 and the C oracle's bit for bit -- for grouped, per-signature and overflowed key grouping, small and
 large batches, valid and corrupted ones, and for batches holding keys missing from the cache (the
-device doubles those 128 times; the host stops splitting until a batch finds every key again)."""
+device doubles those 128 times; the host stops splitting until a batch finds every key again).
+Randomized shapes (test_random_split_vs_oracle): 4 cases by default, EDC_SPLIT_SOAK=<k> for a soak."""
+import os
 import random
 
 import pytest
@@ -164,3 +166,39 @@ def test_split_batch_then_grouped_fallback(cached, register):
                                                          d_msg.data_ptr(), d_off.data_ptr(), bytes([rep + 3]) * 32,
                                                          v, ctypes.byref(cnt), None)
         assert rc == 1 and cnt.value == 4 and list(v.raw) == expect, rep
+
+
+SPLIT_SOAK = int(os.environ.get("EDC_SPLIT_SOAK", "0"))
+
+
+@pytest.mark.parametrize("case", range(SPLIT_SOAK or 4))
+def test_random_split_vs_oracle(cached, oracle_c, case):
+    """random n, key count, grouping mode, window shape and message length; all keys cached, or a
+    random part of them (the device doubles the missing ones 128 times); then the same batch
+    unsplit. Verdict and [8]*check equal the C oracle's each time."""
+    rnd = random.Random(8080 + case)
+    n = rnd.choice([rnd.randrange(1, 400), rnd.randrange(400, 6000), rnd.randrange(6000, 30000)])
+    m = rnd.choice([1, rnd.randrange(1, 300), max(1, n // rnd.choice([1, 3, 40]))])
+    grouping = rnd.choice([0, 0, 1, 2, 3])
+    bits, parts = rnd.choice([(0, 0), (0, 0), (12, 1), (16, 1), (11, 4), (14, 2)])
+    vks, sigs, msgs = _batch(cached, rnd, n, m, msg_len=rnd.randrange(1, 200))
+    bad = rnd.choice([None, rnd.randrange(n)])
+    if bad is not None:
+        msgs[bad] = msgs[bad][:-1] + bytes([msgs[bad][-1] ^ 1])
+    zseed = rnd.randbytes(32)
+    exp = oracle_c.batch_verify(list(zip(vks, sigs, msgs)), zseed)
+    keys = list(dict.fromkeys(vks))
+    if rnd.random() < 0.4 and len(keys) > 1:
+        keys = rnd.sample(keys, rnd.randrange(1, len(keys)))
+    cached.set_key_grouping(grouping)
+    cached.set_msm_shape(bits, parts)
+    tag = (case, n, m, grouping, bits, parts, bad, len(keys))
+    try:
+        _, ok = cached.keycache_load(keys)
+        assert all(ok)
+        for _ in range(2):       # the second run plans from the first one's key counts
+            assert cached.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True) == exp, tag
+        cached.set_key_split(1)
+        assert cached.batch_verify(vks, sigs, msgs, z_seed=zseed, want_check8=True) == exp, tag
+    finally:
+        cached.set_msm_shape(0, 0)
