@@ -138,6 +138,22 @@ constexpr int KEY_ACC_LIMBS = 12;
 // FLAG_KARG: a caller-supplied challenge k (prehashed entries) was not a canonical scalar (>= l):
 // a broken caller contract, reported as EDC_ERR_ARG, never as a verdict.
 enum { FLAG_BAD = 0, FLAG_NKEYS = 1, FLAG_VERDICT = 2, FLAG_OVF = 3, FLAG_UNCACHED = 4, FLAG_KARG = 5, FLAG_COUNT = 8 };
+// A slot's flags array holds FLAG_ALLOC words: [0, FLAG_COUNT) the per-batch flags above (reset by
+// k_init_batch), [FLAG_STAMP0, FLAG_STAMP0 + BST_N) the phase stamps of the EDC_BATCH_STAMPS
+// diagnostic build (make variant VARIANT=bstamps VFLAGS=-DEDC_BATCH_STAMPS, tools/batch_timeline.py):
+// workgroup 0 of each stamped kernel stores the 100 MHz realtime counter as it starts, k_msm_final
+// copies them (and its own end) into words 48.. of the result block. Results are unchanged.
+constexpr int FLAG_ALLOC = 32, FLAG_STAMP0 = 16;
+enum { BST_INIT, BST_COEF, BST_COUNT, BST_DECODE, BST_ACCUM, BST_REDUCE, BST_FINAL, BST_END, BST_N };
+#ifdef EDC_BATCH_STAMPS
+#define BATCH_STAMP(fl, k)                                                                          \
+  do {                                                                                              \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (fl))                                                \
+      const_cast<int*>(fl)[FLAG_STAMP0 + (k)] = (int)__builtin_amdgcn_s_memrealtime();              \
+  } while (0)
+#else
+#define BATCH_STAMP(fl, k) do { } while (0)
+#endif
 
 // Points of a batch MSM: 0 = B, 1..n = R_i, n+1..n+m = the distinct keys (grouped) or each
 // signature's own key (m = n, one key term per signature).
@@ -159,6 +175,10 @@ constexpr int BTAB_ENTRIES = 8;
 constexpr int B256_POS = 32, B256_MULT = 128, B256_ENTRIES = B256_POS * B256_MULT;
 constexpr int BTAB_TOTAL = BTAB_ENTRIES + B256_ENTRIES;
 constexpr uint32_t COEF_CHUNK = 2048;   // signatures per k_coef workgroup (range sizes are multiples)   // context table [1..8]B (per-item fallback, signer)
+
+// Per-batch parameter block of a batch replayed from a captured graph (edc_api.hip, "Graph
+// replays"): the values that change from batch to batch while the launch sequence does not.
+enum { BPAR_SALT = 0, BPAR_SEED = 2, BPAR_ZBASE = 10, BPAR_WORDS = 16 };
 
 // Per-item failure bits written by the prefix kernels (the grouped fallback reads them).
 enum { ITEM_BAD_S = 1, ITEM_BAD_R = 2 };

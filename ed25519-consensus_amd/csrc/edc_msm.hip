@@ -85,6 +85,7 @@ __device__ __forceinline__ void term_digits(const MsmPlan& P, uint32_t t, bool s
 __global__ void __launch_bounds__(256) k_msm_count(MsmPlan P, MsmTerms T, uint32_t per_block,
                                                    uint32_t* __restrict__ counts, const int* __restrict__ flags) {
   extern __shared__ uint32_t hist[];
+  BATCH_STAMP(flags, BST_COUNT);
   const uint32_t nbin = P.nbin();
   for (uint32_t b = threadIdx.x; b < nbin; b += blockDim.x) hist[b] = 0;
   __syncthreads();
@@ -482,8 +483,10 @@ __global__ void __launch_bounds__(256, EDC_ACC_OCC) k_msm_accum_dma(const uint32
                                                                    uint32_t* __restrict__ buckets,
                                                                    uint32_t* __restrict__ heads,
                                                                    uint32_t* __restrict__ slice_W,
-                                                                   uint32_t* __restrict__ slice_T) {
+                                                                   uint32_t* __restrict__ slice_T,
+                                                                   int* __restrict__ stampf) {
   __shared__ uint32_t lend[NSLICE];                 // exclusive end position of each bucket
+  BATCH_STAMP(stampf, BST_ACCUM);
 #ifndef EDC_ACC_LDS_PAD
 #define EDC_ACC_LDS_PAD 0   // measurement knob: extra LDS words per workgroup (caps workgroups per CU)
 #endif
@@ -627,7 +630,9 @@ __device__ __forceinline__ ge_p3 shfl_down_pt(const ge_p3& P, int d) {
 template <int L>
 __global__ void __launch_bounds__(256) k_msm_reduce(uint32_t nbin, const uint32_t* __restrict__ counts,
                                                     const uint32_t* __restrict__ buckets,
-                                                    uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
+                                                    uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T,
+                                                    int* __restrict__ stampf) {
+  BATCH_STAMP(stampf, BST_REDUCE);
   constexpr int CHUNK = NSLICE / L;
   const uint32_t bin = blockIdx.x * (256 / L) + threadIdx.x / L;
   const int j = (int)(threadIdx.x % L);
@@ -693,8 +698,10 @@ constexpr uint32_t REDUCE64_MAX_BINS = EDC_REDUCE64_MAX_BINS;   // 64 lanes per 
 constexpr int REDUCE_WIDE_LANES = EDC_REDUCE_WIDE_LANES;
 __global__ void __launch_bounds__(256) k_msm_reduce_quad(const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ buckets,
-                                                         uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T) {
+                                                         uint32_t* __restrict__ slice_W, uint32_t* __restrict__ slice_T,
+                                                         int* __restrict__ stampf) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  BATCH_STAMP(stampf, BST_REDUCE);
   const uint32_t bin = blockIdx.x;
   if (counts[bin] == 0) return;                     // the accumulation wrote W = T = 0
   const int t = threadIdx.x;
@@ -863,6 +870,7 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
   __shared__ uint32_t blk[64];
   if (blockIdx.x != 0) return;
   __builtin_amdgcn_s_setprio(3);   // a serial chain: issue ahead of co-resident bulk waves
+  BATCH_STAMP(flags, BST_FINAL);
   const RowCtx c = row_ctx();
   const uint32_t wave = threadIdx.x >> 6;
   if (threadIdx.x < 64) blk[threadIdx.x] = 0;
@@ -885,6 +893,10 @@ __global__ void __launch_bounds__(256) k_msm_final(MsmPlan P, const uint32_t* __
     blk[44] = (uint32_t)flags[FLAG_UNCACHED];   // byte 176, after the partial point
     blk[45] = (uint32_t)flags[FLAG_KARG];       // byte 180: a caller's k was not canonical
     if (want_compress) ge_compress(c8, blk + 4);   // bytes 16..48 (little-endian words)
+#ifdef EDC_BATCH_STAMPS
+    for (int k = 0; k < BST_END; ++k) blk[48 + k] = (uint32_t)flags[FLAG_STAMP0 + k];
+    blk[48 + BST_END] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
   }
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -1047,6 +1059,8 @@ extern "C" int edc_debug_set_scatter_stage(uint32_t max_entries) {
   return 0;
 }
 
+uint32_t msm_scatter_stage() { return g_scatter_stage_max; }
+
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed) {
   const uint32_t nbin = P.nbin();
@@ -1114,13 +1128,13 @@ void launch_msm_sort(hipStream_t st, const MsmPlan& P, const uint32_t* counts, c
 void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts, const uint32_t* offsets,
                        const uint2* entries, uint32_t* sorted, uint32_t* bucket_end, const uint32_t* pts,
                        uint32_t* buckets, uint32_t* heads, uint32_t* slice_W, uint32_t* slice_T, int probe_skip,
-                       hipEvent_t acc_begin, hipEvent_t acc_end, bool latency) {
+                       hipEvent_t acc_begin, hipEvent_t acc_end, bool latency, int* stamp_flags) {
   // one workgroup per bin (accumulation of the entries k_msm_sort ordered), then the bin
   // reductions (probe_skip: timing-probe builds only, edc_api.hip EDC_PROBE_SKIP; 0 in the product)
   if (acc_begin) (void)hipEventRecord(acc_begin, st);      // timed batches: the accumulation alone
   if (!(probe_skip & 32))
     hipLaunchKernelGGL(k_msm_accum_dma, dim3(P.nbin()), dim3(256), 0, st, counts, offsets, sorted, bucket_end, pts,
-                       buckets, heads, slice_W, slice_T);
+                       buckets, heads, slice_W, slice_T, stamp_flags);
   if (acc_end) (void)hipEventRecord(acc_end, st);
   if (probe_skip & 64) return;
   // latency: one synchronous batch on an idle GPU (edc_batch_verify*): the quad-cooperative weighted
@@ -1128,13 +1142,14 @@ void launch_msm_bucket(hipStream_t st, const MsmPlan& P, const uint32_t* counts,
   // wave -- a lone wave issues one VALU instruction per ~5.5 cycles whatever its dependencies --
   // at ~2x its VALU work, which only the pipelined submissions (other batches to overlap) mind
   if (P.nbin() <= REDUCE_QUAD_MAX_BINS || (latency && P.nbin() <= REDUCE_QUAD_LATENCY_MAX_BINS))
-    hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T);
+    hipLaunchKernelGGL(k_msm_reduce_quad, dim3(P.nbin()), dim3(256), kReduceLds, st, counts, buckets, slice_W, slice_T,
+                       stamp_flags);
   else if (P.nbin() < REDUCE64_MAX_BINS)
     hipLaunchKernelGGL(k_msm_reduce<64>, dim3(cdiv(P.nbin(), 4)), dim3(256), 0, st, P.nbin(), counts, buckets, slice_W,
-                       slice_T);
+                       slice_T, stamp_flags);
   else
     hipLaunchKernelGGL(k_msm_reduce<REDUCE_WIDE_LANES>, dim3(cdiv(P.nbin(), 256 / REDUCE_WIDE_LANES)), dim3(256), 0, st,
-                       P.nbin(), counts, buckets, slice_W, slice_T);
+                       P.nbin(), counts, buckets, slice_W, slice_T, stamp_flags);
 }
 
 #ifdef EDC_STAMPS
