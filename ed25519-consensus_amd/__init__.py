@@ -52,7 +52,6 @@ ABI_SYMBOLS = [
     "edc_batch_submit_prehashed_device", "edc_batch_verify_prehashed_fallback",
     "edc_batch_verify_prehashed_fallback_device", "edc_multi_route", "edc_multi_debug_force_staged",
     "edc_batch_submit_multi_device", "edc_batch_wait_multi", "edc_combine_records_device", "edc_debug_sc_reduce_wide",
-    "edc_set_graphs", "edc_graph_stats",
 ]
 
 
@@ -209,9 +208,6 @@ def load_library(path=None):
         lib.edc_keycache_size.argtypes = [c_vp]
         lib.edc_set_key_grouping.argtypes = [c_vp, ctypes.c_int]
         lib.edc_set_key_split.argtypes = [c_vp, ctypes.c_int]
-        if hasattr(lib, "edc_set_graphs"):                   # absent from older A/B builds (tools/)
-            lib.edc_set_graphs.argtypes = [c_vp, ctypes.c_int]
-            lib.edc_graph_stats.argtypes = [c_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         if path is None:
             _lib = lib
         return lib
@@ -400,17 +396,6 @@ class Engine:
         """(union-first launches that passed, launches rerun batch by batch) on this context."""
         a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
         self._check(self.lib.edc_multi_union_stats(self.ctx, ctypes.byref(a), ctypes.byref(b)))
-        return a.value, b.value
-
-    def set_graphs(self, mode):
-        """Graph replays of pipelined submissions: True / False, or None for the default
-        (EDC_GRAPHS / the build's)."""
-        self._check(self.lib.edc_set_graphs(self.ctx, -1 if mode is None else (1 if mode else 0)))
-
-    def graph_stats(self):
-        """(launch sequences captured, batches replayed from a captured graph) on this context."""
-        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        self._check(self.lib.edc_graph_stats(self.ctx, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
     def batch_wait(self, ticket, want_check8=False):

@@ -121,14 +121,6 @@ struct Slot {
   int64_t ticket = -1;
   uint32_t probe_runs = 0;      // batches enqueued (EDC_PROBE_SKIP timing builds only)
   uint64_t t_submit_us = 0;     // host time of the submission (EDC_BATCH_STAMPS builds only)
-  // graph replays (pipelined device-input batches): the launch sequence of the last batch shape
-  // captured on this slot, its key, and the parameter block it reads (pinned host copy written
-  // before each replay, device copy filled by k_init_batch)
-  hipGraphExec_t gexec = nullptr;
-  std::vector<uint8_t> gkey;
-  uint32_t* h_par = nullptr;
-  uint32_t* d_par = nullptr;
-  uint64_t greplays = 0, gcaptures = 0;
 };
 
 struct edc_ctx {
@@ -192,8 +184,6 @@ struct edc_ctx {
   int key_split = 0;
   uint32_t last_uncached = 0;
   int multi_union = 1;                  // edc_set_multi_union
-  int graphs = -1;                      // edc_set_graphs: -1 = EDC_GRAPHS / build default, 0 off, 1 on
-  bool graph_broken = false;            // a capture failed: direct launches only
   uint64_t mu_hits = 0, mu_reruns = 0;  // union-first launches that passed / were rerun per batch
   // chunked synchronous host-buffer calls (run_host_chunked): a copy stream and one event per
   // chunk (+ the keys / offsets piece), created on first use
@@ -218,14 +208,7 @@ struct edc_ctx {
     }                                                                   \
   } while (0)
 
-static void drop_graph(Slot& s) {
-  if (s.gexec) (void)hipGraphExecDestroy(s.gexec);
-  s.gexec = nullptr;
-  s.gkey.clear();
-}
-
 static void free_msm_buffers(Slot& s) {
-  drop_graph(s);   // the captured launches name these buffers
   void* ptrs[] = {s.counts, s.offsets, s.cursor, s.slice_W, s.slice_T, s.win, s.buckets, s.heads, s.entries, s.sorted,
                   s.bucket_end};
   for (void* p : ptrs)
@@ -276,8 +259,6 @@ static int init_slot(edc_ctx* ctx, Slot& s) {
   CK(dalloc(&s.d_out, 256 * kMultiMax));
   CK(hipHostMalloc((void**)&s.h_out, 256 * kMultiMax));
   CK(hipHostMalloc((void**)&s.h_acc, 2 * sizeof(uint32_t)));
-  CK(hipHostMalloc((void**)&s.h_par, BPAR_WORDS * sizeof(uint32_t)));
-  CK(dalloc(&s.d_par, BPAR_WORDS));
   for (int p = 0; p <= PH_N; ++p) CK(hipEventCreate(&s.ev[p]));
   for (int p = 0; p < 2; ++p) CK(hipEventCreate(&s.ev_acc[p]));
 #if EDC_DUAL_STREAM
@@ -682,18 +663,6 @@ static uint32_t key_lanes(const edc_ctx* ctx, size_t n, bool per_sig) {
   return (uint32_t)(lanes < n ? lanes : n);
 }
 
-// key-grouping hash salt of the next batch (secret-keyed, a new one per batch); also into the
-// graph parameter block when the batch runs from a captured graph
-static void batch_salt(edc_ctx* ctx, uint32_t salt[2], uint32_t* gpar_h) {
-  const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
-  salt[0] = (uint32_t)h;
-  salt[1] = (uint32_t)(h >> 32);
-  if (gpar_h) {
-    gpar_h[BPAR_SALT] = salt[0];
-    gpar_h[BPAR_SALT + 1] = salt[1];
-  }
-}
-
 // Enqueue the per-signature prefix of the pipeline on slot s: key grouping, SHA-512 challenges,
 // z and coefficients, ZIP215 decode of R_i and the keys. No host synchronization. With d_k (the
 // prehashed entries: the caller's queue-time k, src/batch.rs:76-94) SHA-512 is skipped and the
@@ -701,8 +670,7 @@ static void batch_salt(edc_ctx* ctx, uint32_t salt[2], uint32_t* gpar_h) {
 static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                           const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
                           const uint8_t* d_z, bool with_bin, const MsmPlan* P, bool force_per_sig = false,
-                          bool split = false, const uint32_t* d_k = nullptr, uint32_t* gpar_h = nullptr,
-                          uint32_t* gpar_d = nullptr) {
+                          bool split = false, const uint32_t* d_k = nullptr) {
   if (n >= (1ull << 28)) { ctx->err = "batch too large for one call (max 2^28 items)"; return EDC_ERR_ARG; }
   if (n && (!aligned16(d_vk) || !aligned16(d_sig) || (d_z && !aligned16(d_z)) || (d_k && !aligned16(d_k)))) {
     ctx->err = "device vk / sig / z / k arrays must be 16-byte aligned";
@@ -726,17 +694,13 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   s.per_sig = per_sig;
   s.n_batch = N;
   mark(PH_KEYS);
-  // gpar_h / gpar_d (a launch sequence being captured for graph replays): k_init_batch copies the
-  // pinned parameter block to the device and the key / coefficient kernels read salt, seed and
-  // z base from it, so a replay of the captured sequence runs with the values of its own batch
   launch_init_batch(st, s.flags, per_sig ? (int)N : -1, s.u_acc, s.d_out, per_sig ? nullptr : s.table, per_sig ? 0u : T,
-                    with_bin && EDC_RUN(8) ? s.counts : nullptr, with_bin && EDC_RUN(8) ? P->nbin() : 0u, gpar_h,
-                    gpar_d);
+                    with_bin && EDC_RUN(8) ? s.counts : nullptr, with_bin && EDC_RUN(8) ? P->nbin() : 0u);
   if (!per_sig) {
-    uint32_t salt[2];
-    batch_salt(ctx, salt, gpar_h);
+    const uint64_t h = splitmix64(ctx->secret ^ splitmix64(ctx->nbatches++));
+    const uint32_t salt[2] = {(uint32_t)h, (uint32_t)(h >> 32)};
     launch_keys(st, N, d_vk, s.table, T - 1, salt, ctx->key_grouping == 3, s.slot_key, s.key_slot, s.key_rep,
-                s.key_index, s.key_acc, s.flags, 0xFFFFFFFFu, gpar_d);
+                s.key_index, s.key_acc, s.flags);
   }
   // dual-stream builds (untimed batches): the decode only needs the key grouping, so it runs on
   // the slot's second stream beside SHA-512 / coefficients / binning; its per-item R bits go to
@@ -765,7 +729,7 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   }
   mark(PH_COEF);
   if (EDC_RUN(4)) launch_coef(st, N, d_sig, s.kin, d_z, seed, z_base, s.key_index, s.scal, s.key_acc, s.u_acc, s.itembad, s.flags,
-              per_sig, s.coef_part, split, gpar_d);
+              per_sig, s.coef_part, split);
   mark(PH_MSM_BIN);
   if (with_bin && EDC_RUN(8))
     launch_msm_bin(st, *P, batch_terms(*P, s, N, split), split ? 2 + 3 * N : 1 + 2 * N, s.counts, s.offsets, s.cursor,
@@ -785,54 +749,6 @@ static int enqueue_prefix(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, 
   return 0;
 }
 
-// ---- graph replays (enqueue_batch) ----
-// EDC_GRAPHS=0 / 1 in the environment sets the default; edc_set_graphs overrides it per context
-#ifndef EDC_GRAPHS_DEFAULT
-#define EDC_GRAPHS_DEFAULT 0
-#endif
-static bool graphs_enabled(const edc_ctx* ctx) {
-  static const int env = getenv("EDC_GRAPHS") ? (getenv("EDC_GRAPHS")[0] == '1' ? 1 : 0) : EDC_GRAPHS_DEFAULT;
-  if (ctx->graph_broken) return false;
-  return ctx->graphs < 0 ? env != 0 : ctx->graphs != 0;
-}
-
-template <typename T>
-static void key_put(std::vector<uint8_t>& k, const T& v) {
-  const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
-  k.insert(k.end(), p, p + sizeof(T));
-}
-
-// every value the captured launch sequence of enqueue_batch depends on, other than the parameter
-// block and the slot's own buffers (whose reallocation drops the graph)
-static std::vector<uint8_t> graph_key(const edc_ctx* ctx, const Slot& s, size_t n, const uint8_t* d_vk,
-                                      const uint8_t* d_sig, const uint8_t* d_msg, const uint64_t* d_off,
-                                      const uint8_t* d_z, const uint32_t* d_k, int want_compress, bool latency,
-                                      bool per_sig, bool split, const MsmPlan& P) {
-  std::vector<uint8_t> k;
-  k.reserve(400);
-  key_put(k, (uint64_t)n);
-  const void* ptrs[] = {d_vk, d_sig, d_msg, d_off, d_z, d_k};
-  for (const void* p : ptrs) key_put(k, p);
-  const uint32_t small[] = {(uint32_t)want_compress, (uint32_t)latency, (uint32_t)per_sig, (uint32_t)split,
-                            key_lanes(ctx, n, per_sig), (uint32_t)(ctx->key_grouping == 3),
-                            (uint32_t)(s.probe_runs ? EDC_PROBE_SKIP : 0), msm_scatter_stage()};
-  for (uint32_t v : small) key_put(k, v);
-  key_put(k, P);
-  const KeyCacheView kc = ctx->kc();
-  const void* kp[] = {kc.table, kc.keys, kc.ok, kc.comb, kc.bcomb};
-  for (const void* p : kp) key_put(k, p);
-  const uint32_t kw[] = {kc.tmask, kc.m, kc.s0, kc.s1};
-  for (uint32_t v : kw) key_put(k, v);
-  return k;
-}
-
-// a capture that failed part-way: end it, drop what was captured
-static void end_capture_discard(Slot& s) {
-  hipGraph_t g = nullptr;
-  if (hipStreamEndCapture(s.st, &g) == hipSuccess && g) (void)hipGraphDestroy(g);
-  (void)hipGetLastError();
-}
-
 // Enqueue the whole batch pipeline on slot s (device-resident inputs); no host synchronization.
 static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, const uint8_t* d_sig,
                          const uint8_t* d_msg, const uint64_t* d_off, const uint8_t* z_seed, uint64_t z_base,
@@ -845,50 +761,8 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
   const MsmPlan P = batch_plan(ctx, n, per_sig, split);
   rc = ensure_msm(ctx, s, P, split ? msm_entry_capacity(P, 2 + 3 * n, 0) : msm_entry_capacity(P, n, n + 1));
   if (rc) return rc;
-  // Graph replays: a pipelined slot's batch is ~17 dependent launches, ~90 us of host time per
-  // submission, which a short run of small batches pays before its pipeline fills. The launch
-  // sequence of a batch shape is captured once per slot and replayed with one hipGraphLaunch;
-  // what changes from batch to batch (hash salt, z seed and base) travels in the slot's parameter
-  // block. Everything else the captured launches name is in the key, and any reallocation of the
-  // slot's buffers drops the graph.
-  bool graphed = graphs_enabled(ctx) && !ctx->timing && !s.st2 && n > 0;
-  std::vector<uint8_t> gkey;
-  if (graphed) {
-    gkey = graph_key(ctx, s, n, d_vk, d_sig, d_msg, d_off, d_z, d_k, want_compress, latency, per_sig, split, P);
-    seed_words(z_seed, s.h_par + BPAR_SEED);
-    s.h_par[BPAR_ZBASE] = (uint32_t)z_base;
-    s.h_par[BPAR_ZBASE + 1] = (uint32_t)(z_base >> 32);
-    if (s.gexec && gkey == s.gkey) {
-      // the host state enqueue_prefix and the code below would set
-      s.kin = d_k ? d_k : s.k;
-      s.nmulti = 0;
-      s.timed = false;
-      s.per_sig = per_sig;
-      s.n_batch = (uint32_t)n;
-      if (!per_sig) {
-        uint32_t salt[2];
-        batch_salt(ctx, salt, s.h_par);
-      }
-      CK(hipGraphLaunch(s.gexec, s.st));
-      s.acc_nbin = P.nbin();
-      s.pending = true;
-      s.probe_runs++;
-      s.greplays++;
-      return 0;
-    }
-    drop_graph(s);
-    if (hipStreamBeginCapture(s.st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-      (void)hipGetLastError();      // no capture on this stream: direct launches from now on
-      ctx->graph_broken = true;
-      graphed = false;
-    }
-  }
-  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P, per_sig, split, d_k,
-                      graphed ? s.h_par : nullptr, graphed ? s.d_par : nullptr);
-  if (rc) {
-    if (graphed) end_capture_discard(s);
-    return rc;
-  }
+  rc = enqueue_prefix(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, true, &P, per_sig, split, d_k);
+  if (rc) return rc;
   hipStream_t st = s.st;
   if (s.timed) (void)hipEventRecord(s.ev[PH_MSM_BUCKET], st);
   launch_msm_bucket(st, P, s.counts, s.offsets, s.entries, s.sorted, s.bucket_end, s.pts, s.buckets, s.heads, s.slice_W,
@@ -906,24 +780,6 @@ static int enqueue_batch(edc_ctx* ctx, Slot& s, size_t n, const uint8_t* d_vk, c
       CK(hipMemcpyAsync(s.h_acc, s.offsets + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       CK(hipMemcpyAsync(s.h_acc + 1, s.counts + s.acc_nbin - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     }
-  }
-  if (graphed) {
-    const hipError_t le = hipGetLastError();
-    hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(st, &g);
-    if (e == hipSuccess && le != hipSuccess) e = le;
-    if (e == hipSuccess) e = hipGraphInstantiate(&s.gexec, g, nullptr, nullptr, 0);
-    if (g) (void)hipGraphDestroy(g);
-    if (e != hipSuccess) {
-      // nothing of this batch has run: enqueue it again with direct launches, and keep them
-      s.gexec = nullptr;
-      (void)hipGetLastError();
-      ctx->graph_broken = true;
-      return enqueue_batch(ctx, s, n, d_vk, d_sig, d_msg, d_off, z_seed, z_base, d_z, want_compress, d_k, latency);
-    }
-    s.gkey.swap(gkey);
-    s.gcaptures++;
-    CK(hipGraphLaunch(s.gexec, st));
   }
   CK(hipGetLastError());
   s.pending = true;
@@ -1125,7 +981,6 @@ static int finish_multi(edc_ctx* ctx, Slot& s, size_t nb, int* verdicts, uint8_t
   return any ? EDC_INVALID_SIGNATURE : EDC_OK;
 }
 
-// Wait for slot s and harvest its result block (verdict, bad flag, check8, partial).
 #ifdef EDC_BATCH_STAMPS
 // diagnostic build: one record per waited batch (ticket, n, host submit / wait-return time in us,
 // the device phase stamps of edc_common.h BST_*), read and cleared by edc_debug_batch_stamps
@@ -1142,6 +997,7 @@ extern "C" int edc_debug_batch_stamps(uint32_t* out, size_t cap_words) {
 }
 #endif
 
+// Wait for slot s and harvest its result block (verdict, bad flag, check8, partial).
 static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t partial[128], int* bad_out) {
   if (!s.pending) { ctx->err = "no batch pending in this slot"; return EDC_ERR_ARG; }
   if (s.nmulti) { ctx->err = "multi-batch ticket: wait with edc_batch_wait_multi"; return EDC_ERR_ARG; }
@@ -1543,8 +1399,6 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.flags) (void)hipFree(s.flags);
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.h_out) (void)hipHostFree(s.h_out);
-    if (s.h_par) (void)hipHostFree(s.h_par);
-    if (s.d_par) (void)hipFree(s.d_par);
     if (s.h_acc) (void)hipHostFree(s.h_acc);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
@@ -1562,8 +1416,6 @@ void edc_destroy(edc_ctx* ctx) {
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.h_out) (void)hipHostFree(s.h_out);
     if (s.h_acc) (void)hipHostFree(s.h_acc);
-    if (s.h_par) (void)hipHostFree(s.h_par);
-    if (s.d_par) (void)hipFree(s.d_par);
     for (int p = 0; p <= PH_N; ++p)
       if (s.ev[p]) (void)hipEventDestroy(s.ev[p]);
     for (hipEvent_t e : s.ev_acc)
@@ -1715,24 +1567,6 @@ int edc_batch_wait_multi(edc_ctx* ctx, int64_t ticket, size_t nb, int* verdicts,
   Slot& s = ctx->slot[ticket % ctx->nslots];
   if (!s.pending || s.ticket != ticket) { ctx->err = "unknown or already-waited ticket"; return EDC_ERR_ARG; }
   return finish_multi(ctx, s, nb, verdicts, check8, partials, bad);
-}
-
-int edc_set_graphs(edc_ctx* ctx, int mode) {
-  if (!ctx || mode < -1 || mode > 1) return EDC_ERR_ARG;
-  ctx->graphs = mode;
-  return 0;
-}
-
-int edc_graph_stats(const edc_ctx* ctx, uint64_t* captures, uint64_t* replays) {
-  if (!ctx) return EDC_ERR_ARG;
-  uint64_t c = 0, r = 0;
-  for (const Slot& s : ctx->slot) {
-    c += s.gcaptures;
-    r += s.greplays;
-  }
-  if (captures) *captures = c;
-  if (replays) *replays = r;
-  return 0;
 }
 
 int edc_set_multi_union(edc_ctx* ctx, int on) {

@@ -176,10 +176,6 @@ constexpr int B256_POS = 32, B256_MULT = 128, B256_ENTRIES = B256_POS * B256_MUL
 constexpr int BTAB_TOTAL = BTAB_ENTRIES + B256_ENTRIES;
 constexpr uint32_t COEF_CHUNK = 2048;   // signatures per k_coef workgroup (range sizes are multiples)   // context table [1..8]B (per-item fallback, signer)
 
-// Per-batch parameter block of a batch replayed from a captured graph (edc_api.hip, "Graph
-// replays"): the values that change from batch to batch while the launch sequence does not.
-enum { BPAR_SALT = 0, BPAR_SEED = 2, BPAR_ZBASE = 10, BPAR_WORDS = 16 };
-
 // Per-item failure bits written by the prefix kernels (the grouped fallback reads them).
 enum { ITEM_BAD_S = 1, ITEM_BAD_R = 2 };
 

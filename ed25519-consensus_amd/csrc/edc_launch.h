@@ -20,15 +20,12 @@ void launch_decompress_range(hipStream_t st, uint32_t n, uint32_t r0, uint32_t r
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
                  uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags,
-                 uint32_t kcap = 0xFFFFFFFFu, const uint32_t* par = nullptr);
+                 uint32_t kcap = 0xFFFFFFFFu);
 // per-signature key terms (no grouping): m = n, key j is signature j's own key (key_rep = null)
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig, uint32_t* coef_part, bool split = false, const uint32_t* par = nullptr);
-// par (launch_keys, launch_coef): a batch parameter block in device memory (BPAR_*, written by
-// k_init_batch from the host's pinned copy) that overrides salt / seed / zbase, so that a captured
-// graph of the batch replays with new values
+                 bool per_sig, uint32_t* coef_part, bool split = false);
 // launch_coef in pieces (chunked host-buffer calls): the per-item pass over items
 // [item0, item0 + cnt) (item0 a multiple of COEF_CHUNK) as each chunk lands, then once the
 // per-key merge and the coefficient reduction
@@ -64,10 +61,8 @@ void launch_expand_keys(hipStream_t st, uint32_t n, const uint32_t* key_idx, con
                         const uint32_t* keys, uint8_t* vk_out);
 // per-batch resets in one launch: flags (FLAG_NKEYS = nkeys if >= 0), u_acc, the 256-byte result
 // block, table[0..T) = 0xFFFFFFFF, counts[0..nbin) = 0 (T / nbin may be 0)
-// hpar / dpar (graph replays): copy the BPAR_WORDS-word parameter block hpar (pinned host) to dpar
 void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long* u_acc, uint8_t* d_out, uint32_t* table,
-                       uint32_t T, uint32_t* counts, uint32_t nbin, const uint32_t* hpar = nullptr,
-                       uint32_t* dpar = nullptr);
+                       uint32_t T, uint32_t* counts, uint32_t nbin);
 // edc_msm.hip: per-device kernel attributes (the scatter's dynamic LDS beyond 64 KB); call on
 // every device a context uses, after hipSetDevice
 hipError_t msm_init_device();
@@ -102,8 +97,6 @@ void launch_copy_block(hipStream_t st, const uint8_t* src, uint8_t* dst);
 // g shard result blocks (256 bytes each, device) -> verdict block (as launch_combine)
 void launch_combine_blocks(hipStream_t st, uint32_t g, const uint8_t* blocks, int want_compress, uint8_t* out);
 size_t msm_entry_capacity(const MsmPlan& P, size_t short_terms, size_t full_terms);
-// the scatter's LDS stage cap in force (edc_debug_set_scatter_stage): part of a batch graph's key
-uint32_t msm_scatter_stage();
 // edc_single.hip
 void launch_init_btable(hipStream_t st, uint32_t* btab);
 void launch_verify_single(hipStream_t st, uint32_t n, const uint8_t* vk, const uint8_t* sig,

@@ -1059,8 +1059,6 @@ extern "C" int edc_debug_set_scatter_stage(uint32_t max_entries) {
   return 0;
 }
 
-uint32_t msm_scatter_stage() { return g_scatter_stage_max; }
-
 void launch_msm_bin(hipStream_t st, const MsmPlan& P, const MsmTerms& T, uint32_t max_terms, uint32_t* counts,
                     uint32_t* offsets, uint32_t* cursor, uint2* entries, const int* flags, bool counts_zeroed) {
   const uint32_t nbin = P.nbin();

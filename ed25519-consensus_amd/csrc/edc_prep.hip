@@ -350,9 +350,8 @@ __global__ void __launch_bounds__(256) k_key_insert(uint32_t n, const uint8_t* _
                                                     uint32_t* __restrict__ key_slot_of_sig,
                                                     uint32_t* __restrict__ key_rep,
                                                     unsigned long long* __restrict__ key_acc,
-                                                    int* __restrict__ flags, const uint32_t* __restrict__ par) {
+                                                    int* __restrict__ flags) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (par) { salt0 = par[BPAR_SALT]; salt1 = par[BPAR_SALT + 1]; }
   if (i < n) key_insert_one(i, vk, table, tmask, salt0, salt1, probe_cap, slot_key, key_slot_of_sig, key_rep,
                             key_acc, flags);
 }
@@ -370,9 +369,8 @@ __global__ void __launch_bounds__(256) k_key_seed(uint32_t n, const uint8_t* __r
                                                   uint32_t* __restrict__ key_slot_of_sig,
                                                   uint32_t* __restrict__ key_rep,
                                                   unsigned long long* __restrict__ key_acc,
-                                                  int* __restrict__ flags, const uint32_t* __restrict__ par) {
+                                                  int* __restrict__ flags) {
   const uint32_t i = (uint32_t)(((uint64_t)(blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u) % n);
-  if (par) { salt0 = par[BPAR_SALT]; salt1 = par[BPAR_SALT + 1]; }
   key_insert_one(i, vk, table, tmask, salt0, salt1, probe_cap, slot_key, key_slot_of_sig, key_rep, key_acc, flags);
 }
 
@@ -446,16 +444,11 @@ __global__ void __launch_bounds__(256) k_coef(uint32_t n, const uint8_t* __restr
                                               uint8_t* __restrict__ itembad,
                                               int* __restrict__ flags, int per_sig_host, uint32_t rsize, uint32_t m,
                                               uint32_t* __restrict__ coef_part, int split, uint32_t item0,
-                                              uint32_t iend, const uint32_t* __restrict__ par) {
+                                              uint32_t iend) {
   __shared__ uint32_t tag[COEF_SLOTS];
   __shared__ unsigned long long acc[COEF_SLOTS][PL];
   __shared__ unsigned long long red[4][PL];
   BATCH_STAMP(flags, BST_COEF);
-  if (par) {        // a batch replayed from a captured graph: z seed and base from its parameter block
-#pragma unroll
-    for (int j = 0; j < 8; ++j) seed.w[j] = par[BPAR_SEED + j];
-    zbase = (uint64_t)par[BPAR_ZBASE] | ((uint64_t)par[BPAR_ZBASE + 1] << 32);
-  }
   const bool per_sig = per_sig_host || flags[FLAG_OVF];
   for (int s = threadIdx.x; s < COEF_SLOTS; s += blockDim.x) {
     tag[s] = 0xFFFFFFFFu;
@@ -788,16 +781,15 @@ void launch_decompress(hipStream_t st, uint32_t n, const uint8_t* sig, const uin
 }
 void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table, uint32_t tmask,
                  const uint32_t salt[2], bool force_overflow, uint32_t* slot_key, uint32_t* key_slot_of_sig,
-                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags, uint32_t kcap,
-                 const uint32_t* par) {
+                 uint32_t* key_rep, uint32_t* key_index, unsigned long long* key_acc, int* flags, uint32_t kcap) {
   if (!n) return;
   const uint32_t cap = force_overflow ? 0u : KEY_PROBE_CAP;
   if (n > 4 * KEY_SEED_SAMPLE) {
     hipLaunchKernelGGL(k_key_seed, dim3(KEY_SEED_SAMPLE / 256), dim3(256), 0, st, n, vk, table, tmask,
-                       salt[0], salt[1], cap, slot_key, key_slot_of_sig, key_rep, key_acc, flags, par);
+                       salt[0], salt[1], cap, slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   }
   hipLaunchKernelGGL(k_key_insert, dim3(cdiv(n, 256)), dim3(256), 0, st, n, vk, table, tmask, salt[0], salt[1], cap,
-                     slot_key, key_slot_of_sig, key_rep, key_acc, flags, par);
+                     slot_key, key_slot_of_sig, key_rep, key_acc, flags);
   hipLaunchKernelGGL(k_key_index, dim3(cdiv(n, 256)), dim3(256), 0, st, n, key_slot_of_sig, slot_key,
                      key_index, flags, kcap);
 }
@@ -806,13 +798,9 @@ void launch_keys(hipStream_t st, uint32_t n, const uint8_t* vk, uint32_t* table,
 // the latency of a small batch.
 __global__ void __launch_bounds__(256) k_init_batch(int* __restrict__ flags, int nkeys, unsigned long long* __restrict__ u_acc,
                                                     uint32_t* __restrict__ d_out, uint32_t* __restrict__ table, uint32_t T,
-                                                    uint32_t* __restrict__ counts, uint32_t nbin,
-                                                    const uint32_t* __restrict__ hpar, uint32_t* __restrict__ dpar) {
+                                                    uint32_t* __restrict__ counts, uint32_t nbin) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   BATCH_STAMP(flags, BST_INIT);
-  // graph replays: the batch's parameter block, written by the host into pinned memory before the
-  // launch, copied to device memory for the later kernels of the batch (one read over PCIe)
-  if (hpar && i < BPAR_WORDS) dpar[i] = __hip_atomic_load(hpar + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (i < FLAG_COUNT) flags[i] = (i == FLAG_NKEYS && nkeys >= 0) ? nkeys : 0;
   if (i < KEY_ACC_LIMBS) u_acc[i] = 0;
   if (i < 64) d_out[i] = 0;
@@ -821,25 +809,25 @@ __global__ void __launch_bounds__(256) k_init_batch(int* __restrict__ flags, int
 }
 
 void launch_init_batch(hipStream_t st, int* flags, int nkeys, unsigned long long* u_acc, uint8_t* d_out, uint32_t* table,
-                       uint32_t T, uint32_t* counts, uint32_t nbin, const uint32_t* hpar, uint32_t* dpar) {
+                       uint32_t T, uint32_t* counts, uint32_t nbin) {
   const uint32_t work = T > nbin ? T : nbin;
   uint32_t grid = cdiv(work > 256 ? work : 256, 256);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(k_init_batch, dim3(grid), dim3(256), 0, st, flags, nkeys, u_acc, reinterpret_cast<uint32_t*>(d_out),
-                     table, T, counts, nbin, hpar, dpar);
+                     table, T, counts, nbin);
 }
 
 void launch_coef(hipStream_t st, uint32_t n, const uint8_t* sig, const uint32_t* k, const uint8_t* zexp,
                  const uint32_t seed[8], uint64_t zbase, const uint32_t* key_index, uint32_t* scal,
                  unsigned long long* key_acc, unsigned long long* u_acc, uint8_t* itembad, int* flags,
-                 bool per_sig, uint32_t* coef_part, bool split, const uint32_t* par) {
+                 bool per_sig, uint32_t* coef_part, bool split) {
   seed8 s;
   for (int j = 0; j < 8; ++j) s.w[j] = seed[j];
   if (n) {
     const uint32_t nwg = cdiv(n, COEF_CHUNK);
     uint32_t* part = per_sig ? nullptr : coef_part;
     hipLaunchKernelGGL(k_coef, dim3(nwg), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index, scal, key_acc,
-                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part, split ? 1 : 0, 0u, n, par);
+                       u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, part, split ? 1 : 0, 0u, n);
   }
   launch_coef_finish(st, n, key_acc, u_acc, scal, flags, per_sig, coef_part, split);
 }
@@ -852,7 +840,7 @@ void launch_coef_range(hipStream_t st, uint32_t n, uint32_t item0, uint32_t cnt,
   if (cnt)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(cnt, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase, key_index,
                        scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, 0u, 0u, per_sig ? nullptr : coef_part,
-                       split ? 1 : 0, item0, item0 + cnt, (const uint32_t*)nullptr);
+                       split ? 1 : 0, item0, item0 + cnt);
 }
 void launch_coef_finish(hipStream_t st, uint32_t n, unsigned long long* key_acc, unsigned long long* u_acc,
                         uint32_t* scal, int* flags, bool per_sig, uint32_t* coef_part, bool split) {
@@ -878,7 +866,7 @@ void launch_range_coef(hipStream_t st, uint32_t n, uint32_t rsize, uint32_t nran
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, zexp, s, zbase,
                        key_index, scal, key_acc, u_acc, (uint8_t*)nullptr, flags, per_sig ? 1 : 0, rsize, mm,
-                       (uint32_t*)nullptr, 0, 0u, n, (const uint32_t*)nullptr);
+                       (uint32_t*)nullptr, 0, 0u, n);
   hipLaunchKernelGGL(k_range_terms, dim3(grid_cap(cdiv((uint64_t)nranges * (mm + 1), 256), 1024)), dim3(256), 0, st,
                      n, nranges, mm, key_acc, u_acc, xpt, xrg, xscal);
 }
@@ -893,7 +881,7 @@ void launch_multi_coef(hipStream_t st, uint32_t n, uint32_t nr, uint32_t kstride
   if (n)
     hipLaunchKernelGGL(k_coef, dim3(cdiv(n, COEF_CHUNK)), dim3(256), 0, st, n, sig, k, (const uint8_t*)nullptr, s, zbase,
                        key_index, scal, key_acc, u_acc, itembad, flags, per_sig ? 1 : 0, n / nr, kstride,
-                       (uint32_t*)nullptr, 0, 0u, n, (const uint32_t*)nullptr);
+                       (uint32_t*)nullptr, 0, 0u, n);
   hipLaunchKernelGGL(k_multi_terms, dim3(grid_cap(cdiv((uint64_t)nr * (per_sig ? 1 : kstride + 1), 256), 1024)),
                      dim3(256), 0, st, n, nr, kstride, key_acc, u_acc, flags, per_sig ? 1 : 0, xpt, xrg, xscal);
 }

@@ -105,18 +105,6 @@ int64_t edc_batch_submit_device(edc_ctx* ctx, size_t n, const uint8_t* d_vk, con
 int edc_batch_wait(edc_ctx* ctx, int64_t ticket, uint8_t check8[32], uint8_t partial[128], int* bad);
 
 /*
- * Graph replays of pipelined submissions (edc_batch_submit_device / _prehashed_device / the
- * host-buffer submit forms): each slot captures the launch sequence of its batch shape once and
- * replays it with one hipGraphLaunch while the shape (n, input pointers, MSM plan, key cache, ...)
- * stays the same; the per-batch values (hash salt, z seed and base) reach the replay through a
- * parameter block. Same kernels, same arguments: results are identical either way.
- * mode: 1 on, 0 off, -1 the default (environment EDC_GRAPHS=0/1, else the build's default).
- * edc_graph_stats: captures and replays over the context's slots so far.
- */
-int edc_set_graphs(edc_ctx* ctx, int mode);
-int edc_graph_stats(const edc_ctx* ctx, uint64_t* captures, uint64_t* replays);
-
-/*
  * Several consecutive batches in ONE launch sequence (a node verifying several blocks' votes at
  * once, or one GPU's shards of consecutive blocks; reference src/batch.rs:149-217 once per batch):
  * nb (1..16) batches of n_per items each (n_per a multiple of 2048), back to back in device
