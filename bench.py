@@ -485,9 +485,8 @@ def main(argv=None):
     eng._check(lib.edc_set_msm_shape(eng.ctx, args.window_bits, args.msm_parts))
     eng._check(lib.edc_set_msm_bin_entries(eng.ctx, args.bin_entries))
     eng._check(lib.edc_reserve(eng.ctx, n))        # every in-flight slot's workspace, before any step
-    if ring is not None:                          # communicator set-up stays out of the timed region
-        ring.post(bytes(129))                     # even with --warmup 0
-        ring.pop()
+    if ring is not None:                          # communicator and per-buffer set-up stay out of the
+        ring.warm()                               # timed region, even with --warmup 0
         ring.post, ring.pop = timed_ring_op(ring.post, "post"), timed_ring_op(ring.pop, "pop")
 
     def timed(k):

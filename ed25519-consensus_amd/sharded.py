@@ -128,6 +128,19 @@ class ExchangeRing:
     def __len__(self):
         return len(self.pending) + sum(cnt - done for _, cnt, _, done in self.sent)
 
+    def warm(self):
+        """Set-up outside a timed region: one full group through EVERY staging buffer at once (the
+        free list is LIFO, so a single post/pop would only ever touch one of them). The first
+        collective on each buffer pays the backend's per-buffer set-up (RCCL), which otherwise lands
+        in the first timed batches. Every rank must call it (it runs collectives); the records are
+        zeros and their results are discarded."""
+        assert not self.pending and not self.sent, "ExchangeRing.warm: exchanges in flight"
+        for _ in range(len(self.bufs)):
+            for _ in range(self.K):
+                self.post(bytes(self.n))
+        while len(self):
+            self.pop()
+
     def post(self, rec):
         assert len(rec) == self.n
         self.pending.append(bytes(rec))

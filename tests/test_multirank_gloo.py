@@ -199,3 +199,34 @@ def test_exchange_ring_pop_without_post():
         assert len(ring) == 0
     finally:
         dist.destroy_process_group()
+
+
+def test_exchange_ring_warm_uses_every_buffer():
+    """ExchangeRing.warm (bench.py, before timing): one group through every staging buffer at once
+    -- a single post / pop would reuse one buffer (LIFO free list) and leave the others' first
+    collective inside the timed region -- then an empty ring that exchanges records as before."""
+    import torch
+    import torch.distributed as dist
+    import importlib
+    from conftest import load_pkg
+    load_pkg()
+    sharded = importlib.import_module("ed25519_consensus_amd.sharded")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ring = sharded.ExchangeRing(dist, torch.device("cpu"), depth=8, group=4)
+        in_flight, send = [], ring._send
+
+        def spy():
+            send()
+            in_flight.append(len(ring.sent))
+        ring._send = spy
+        ring.warm()
+        assert max(in_flight) == len(ring.bufs) == 4
+        assert len(ring) == 0 and sorted(ring.free) == list(range(len(ring.bufs)))
+        recs = [bytes([i]) * 129 for i in range(6)]
+        for r in recs:
+            ring.post(r)
+        assert [ring.pop() for _ in recs] == [[r] for r in recs]
+    finally:
+        dist.destroy_process_group()
