@@ -220,6 +220,9 @@ __device__ __noinline__ ge_niels shift128_niels(ge_p3 P) {
 // call decodes each chunk's R as it lands and the keys once the key grouping is done). The key
 // count m is only known on the device: the host sizes klanes from the previous grouped batch, and
 // a lane decodes keys j, j + klanes, ... when m is larger.
+#ifndef EDC_DEC_LDS_PAD
+#define EDC_DEC_LDS_PAD 0
+#endif
 #ifndef EDC_DEC_OCC
 #define EDC_DEC_OCC 4   // waves per SIMD the decode is compiled for (128 VGPRs; 5 -> 96 with spills outside the squaring loops)
 #endif
@@ -232,6 +235,12 @@ __global__ void __launch_bounds__(256, EDC_DEC_OCC) k_decompress(uint32_t n, uin
                                                        KeyCacheView kcache, int split) {
   const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
   BATCH_STAMP(flags, BST_DECODE);
+#if EDC_DEC_LDS_PAD
+  // measurement knob: LDS the decode never reads, so that at most 160 KB / pad decode workgroups
+  // share a CU and the rest of its VGPRs stay free for the other batches' kernels
+  __shared__ uint32_t dec_pad[EDC_DEC_LDS_PAD / 4];
+  asm volatile("" :: "v"(dec_pad));
+#endif
   uint32_t w[8];
   if (lane < rcnt) {
     const uint32_t i = r0 + lane;
