@@ -142,7 +142,7 @@ for step in "$@"; do
           for c in ${AB_CONFIGS:-c3 n17 c2 c5}; do
             case $c in
               c3) a="--steps 40";; c2) a="--config c2 --steps 40";; c5) a="--config c5 --steps 12";;
-              n17) a="--n 131072 --steps 40";; driver) a="--steps 20";; *) a="$c";;
+              n17) a="--n 131072 --steps 40";; n17x20) a="--n 131072 --steps 20";; driver) a="--steps 20";; *) a="$c";;
             esac
             run ab 300 python3 -u bench.py $a --warmup 5 --no-cpu-baseline --profile-steps 1 --lib "$PWD/$lib"
             summ "$(log ab)" "$c-$v" | tee -a "gpurun_out/${tag}_ab_summary.log"
