@@ -985,11 +985,13 @@ static int finish_multi(edc_ctx* ctx, Slot& s, size_t nb, int* verdicts, uint8_t
 // diagnostic build: one record per waited batch (ticket, n, host submit / wait-return time in us,
 // the device phase stamps of edc_common.h BST_*), read and cleared by edc_debug_batch_stamps
 static std::vector<uint32_t> g_bstamps;
+static std::mutex g_bstamps_mu;    // contexts on several threads share the log
 static uint64_t host_us() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 extern "C" int edc_debug_batch_stamps(uint32_t* out, size_t cap_words) {
+  std::lock_guard<std::mutex> g(g_bstamps_mu);
   const size_t n = std::min(cap_words, g_bstamps.size());
   if (out) memcpy(out, g_bstamps.data(), n * sizeof(uint32_t));
   g_bstamps.clear();
@@ -1014,6 +1016,7 @@ static int finish_batch(edc_ctx* ctx, Slot& s, uint8_t check8[32], uint8_t parti
   const int bad = reinterpret_cast<int*>(s.h_out)[1];
 #ifdef EDC_BATCH_STAMPS
   if (&s != &ctx->comb) {
+    std::lock_guard<std::mutex> g(g_bstamps_mu);
     g_bstamps.push_back((uint32_t)s.ticket);
     g_bstamps.push_back(s.n_batch);
     g_bstamps.push_back((uint32_t)s.t_submit_us);
