@@ -239,6 +239,15 @@ def launch_ranks(argv, nranks, call=None):
     return call(rank_launch_cmd(argv, nranks, free_port()), env=env)
 
 
+def default_inflight(n, small_depth):
+    """Batches in flight for n signatures per GPU: 6 from 2^20 (6 and 7 alternate within the spread
+    there), 7 for 2^19 shards (+1.5 % over 6 in 4 of 4 alternating pairs, profiles/r06/r06zn_*),
+    small_depth below (16 on one rank, 12 beside RCCL's and the exchange ring's queues)."""
+    if n >= (1 << 20):
+        return 6
+    return 7 if n >= (1 << 19) else small_depth
+
+
 def world_error(gpus, world, backend, local_world, ndev):
     """Why this rank must not run (None if it may): the process group must be exactly the --gpus
     ranks asked for, and with RCCL every local rank needs a GPU of its own (the gloo rehearsal
@@ -276,7 +285,8 @@ def main(argv=None):
     ap.add_argument("--profile-steps", type=int, default=3, help="extra instrumented steps for per-phase timings")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight per GPU (submit/wait pipelining, <= the context's 16 slots); "
-                         "0 = 6 from 2^19 signatures per GPU up, 16 below (small shards need more overlap)")
+                         "0 = 6 from 2^20 signatures per GPU up, 7 from 2^19, 16 below (small shards need "
+                         "more overlap; 12 in a multi-rank run)")
     ap.add_argument("--keycache", action="store_true",
                     help="register the validator keys in the context's key cache before timing (edc_keycache_load)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
@@ -375,7 +385,7 @@ def main(argv=None):
             # union first measured 6.38e8 at 3 and 5.55e8 at 6 at 8 x 2^17, profiles/r04/r04w_union_inflight6_summary.log)
             args.inflight = 3 if n * nmb >= (1 << 19) else 4
         else:
-            args.inflight = 6 if n >= (1 << 19) else small_depth
+            args.inflight = default_inflight(n, small_depth)
     args.inflight = min(args.inflight, slots)
     if nmb > 1:    # every slot's multi-batch workspace is allocated on its first launch: warm them all
         args.warmup = max(args.warmup, args.inflight + 1)
@@ -520,7 +530,7 @@ def main(argv=None):
         n = args.n if args.scaling == "strong" else args.n // world
         base = rank * n
         if inflight_auto:              # the in-flight depth the default picks for this shard size
-            args.inflight = min(6 if n >= (1 << 19) else small_depth, slots)
+            args.inflight = min(default_inflight(n, small_depth), slots)
             eng._check(lib.edc_set_slots(eng.ctx, args.inflight))
         eng._check(lib.edc_reserve(eng.ctx, n))
         main_data = (vk, sig, msg, off)

@@ -87,3 +87,14 @@ def test_launched_ranks_fail_fast_without_gpus():
     assert r.returncode != 0
     assert "GPU(s) visible" in r.stderr
     assert r.stdout.strip() == ""        # no JSON line from a refused run
+
+
+def test_default_inflight_by_shard_size():
+    """batches in flight per GPU by signatures per GPU: the N = 1 headline (2^20) and the 2-, 4-
+    and 8-rank strong shards (2^19, 2^18, 2^17; small shards keep 12 beside RCCL, 16 alone)"""
+    assert bench.default_inflight(1 << 21, 12) == 6
+    assert bench.default_inflight(1 << 20, 16) == 6
+    assert bench.default_inflight(1 << 19, 12) == 7
+    assert bench.default_inflight((1 << 19) + 5, 16) == 7
+    assert bench.default_inflight(1 << 18, 12) == 12
+    assert bench.default_inflight(1 << 17, 16) == 16
