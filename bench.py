@@ -311,6 +311,10 @@ def main(argv=None):
                     help="multi-rank: batches whose exchange is in flight before the oldest verdict is completed")
     ap.add_argument("--exchange-group", type=int, default=4,
                     help="multi-rank: batches whose records leave in one all-gather (sharded.ExchangeRing)")
+    ap.add_argument("--spinup-ms", type=float, default=100.0,
+                    help="device set-up before the warmup steps: run this workload's batches for this many "
+                         "milliseconds (rank-local), so that the timed steps meet the GPU at its sustained "
+                         "rate and not on its way up from idle (0 = none; reported as `spinup` in the line)")
     ap.add_argument("--lib", default=None, help="tools/ab_variants.sh only: load this A/B build of libedc.so")
     args = ap.parse_args(argv)
     if args.gpus < 1:
@@ -516,11 +520,41 @@ def main(argv=None):
             el = float(tt.item())
         return el, codes
 
+    spin = {"ms": 0.0, "batches": 0}
+
+    def spin_up(ms):
+        """Device set-up before the warmup steps: batches of this workload, rank-local (no
+        collectives, so ranks need not agree on a count), for `ms` milliseconds. From idle the GPU
+        needs ~50 ms of load before it runs at its sustained rate: the first 20 timed steps after
+        only the 5 warmup steps measured 6.70-6.71e8 (2^20) and 4.53-4.70e8 (2^17 shards), after a
+        50-800 ms spin-up 6.96-7.07e8 and 5.1-5.4e8 (profiles/r06/r06zq_*, r06zr_*)."""
+        if ms <= 0:
+            return
+        t_spin = time.perf_counter()
+        while True:
+            if len(pending) >= max(1, args.inflight):
+                wait_oldest()()
+            submit()
+            spin["batches"] += 1
+            if (time.perf_counter() - t_spin) * 1e3 >= ms:
+                break
+        while pending:
+            wait_oldest()()
+        spin["ms"] += round((time.perf_counter() - t_spin) * 1e3, 1)
+
+    spin_up(args.spinup_ms)
     run_steps(args.warmup)
     for key in xstat:
         xstat[key] = 0.0
     elapsed, codes = timed(args.steps)
     exchange_us = {key: round(v / max(1, args.steps) * 1e6, 1) for key, v in xstat.items()}
+    # diagnostic only (EDC_TIMED_REPEATS=r): the same timed region r - 1 more times right after
+    # the first, reported beside it; `value` is always the first
+    again = []
+    for _ in range(int(os.environ.get("EDC_TIMED_REPEATS", "1")) - 1):
+        el_r, codes_r = timed(args.steps)
+        assert all(c == 0 for c in codes_r) or args.lib, f"valid synthetic batch rejected: {codes_r}"
+        again.append(round(n * nmb * world * args.steps / el_r, 1))
     other = None
     if dist and nmb == 1 and not args.prehashed:
         # multi-rank: the other scaling shape beside the headline one, on the same ranks and data
@@ -540,6 +574,7 @@ def main(argv=None):
         # as many signatures as the headline run (steps x n_main / n): a short run of small
         # batches is mostly the pipeline's fill and drain (16 batches in flight)
         k2 = max(args.steps, round(args.steps * n_main / max(1, n)))
+        spin_up(args.spinup_ms)
         run_steps(max(2, args.warmup))
         el2, codes2 = timed(k2)
         other = {"scaling": "weak" if args.scaling == "strong" else "strong", "sigs_per_gpu": n,
@@ -668,6 +703,11 @@ def main(argv=None):
                                        "completing it (waits for the collective), combining the partials"}
                      if dist else None),
             "scaling_other_shape": other,
+            "timed_repeats": again or None,
+            # device set-up before the warmup steps (--spinup-ms): batches of this workload, untimed
+            "spinup": {"ms": spin["ms"], "batches": spin["batches"],
+                       "note": "untimed batches of this workload before the warmup steps: from idle the GPU needs "
+                               "~50 ms of load to reach its sustained rate (profiles/r06/r06zr_spinup_sweep.log)"},
             "roofline": {"bound": "valu_int", "kernel": "k_decompress (R_i)",
                          "achieved": round(achieved, 3), "peak": round(PEAK_TMAD, 2),
                          "unit": "T v_mad_u64_u32/s", "frac": round(achieved / PEAK_TMAD, 4),
