@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU-box: forced single-rank RCCL loop at 2^17 x 20 with RCCL's streams at high priority
+# (TORCH_NCCL_HIGH_PRIORITY=1, bench.py's default) or normal (0), alternating, plus one rank
+# without a process group.
+set -o pipefail
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+tag=${1:-prio}
+for rep in 1 2 3; do
+  for p in 1 0 plain; do
+    log=gpurun_out/${tag}_p${p}_$rep.log
+    if [ $p = plain ]; then
+      timeout -k 10 300 python3 -u bench.py --n 131072 --steps 20 --warmup 5 --no-cpu-baseline --no-host-api --profile-steps 1 > $log 2>&1 || { tail -5 $log; exit 1; }
+    else
+      TORCH_NCCL_HIGH_PRIORITY=$p EDC_FORCE_DIST=1 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port $((29850 + rep * 10 + ${p/plain/9})) bench.py --batch 131072 --steps 20 \
+        --warmup 5 --no-cpu-baseline --no-host-api --profile-steps 1 > $log 2>&1 || { tail -5 $log; exit 1; }
+    fi
+    python3 -c "import json; d=json.loads([l for l in open('$log') if l.startswith('{')][-1]); o=d['scaling_other_shape'] or {}; print('prio $p rep $rep', d['value'], d['ms_per_step'], 'repeat', o.get('value'))" | tee -a gpurun_out/${tag}_ab.log
+  done
+done
