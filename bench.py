@@ -462,11 +462,14 @@ def main(argv=None):
         rc = eng._check(lib.edc_batch_wait(eng.ctx, pending.pop(0), None, None, None))
         return lambda: rc
 
+    tail = {"t_wait": 0.0, "split": None}    # multi-rank: where the timed region's tail goes
+
     def wait_partial(t):
         """multi-GPU: this rank's partial point of the global batch (and its reject flag)"""
         part = ctypes.create_string_buffer(128)
         bad = ctypes.c_int(0)
         eng._check(lib.edc_batch_wait(eng.ctx, t, None, part, ctypes.byref(bad)))
+        tail["t_wait"] = time.perf_counter()
         return part.raw, bad.value
 
     def submit_ticket():
@@ -510,10 +513,17 @@ def main(argv=None):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         codes = run_steps(k)
+        t1 = time.perf_counter()
         torch.cuda.synchronize()
+        t2 = time.perf_counter()
         if dist:
             dist.barrier()
         el = time.perf_counter() - t0
+        if dist and tail["split"] is None:
+            # after the last batch's partial: completing the exchanges still in flight, then the
+            # closing device sync and barrier (fixed per timed region, not per batch)
+            tail["split"] = {"exchange_drain": round((t1 - tail["t_wait"]) * 1e6, 1),
+                             "sync": round((t2 - t1) * 1e6, 1), "barrier": round((t0 + el - t2) * 1e6, 1)}
         if dist:
             tt = torch.tensor([el], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -698,9 +708,10 @@ def main(argv=None):
             # the process group the ranks actually formed (None: one process, no collectives)
             "comm": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                       "exchange_lag": args.exchange_lag, "exchange_group": args.exchange_group,
-                      "exchange_us": exchange_us,
+                      "exchange_us": exchange_us, "timed_tail_us": tail["split"],
                       "exchange_note": "host time per batch inside the timed loop: posting the all-gather, "
-                                       "completing it (waits for the collective), combining the partials"}
+                                       "completing it (waits for the collective), combining the partials; timed_tail_us: the "
+                                       "headline region's end after the last batch's partial"}
                      if dist else None),
             "scaling_other_shape": other,
             "timed_repeats": again or None,
