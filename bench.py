@@ -242,7 +242,7 @@ def launch_ranks(argv, nranks, call=None):
 def default_inflight(n, small_depth):
     """Batches in flight for n signatures per GPU: 6 from 2^20 (6 and 7 alternate within the spread
     there), 7 for 2^19 shards (+1.5 % over 6 in 4 of 4 alternating pairs, profiles/r06/r06zn_*),
-    small_depth below (16 on one rank, 12 beside RCCL's and the exchange ring's queues)."""
+    small_depth below (16, on one rank and beside RCCL's and the exchange ring's queues)."""
     if n >= (1 << 20):
         return 6
     return 7 if n >= (1 << 19) else small_depth
@@ -380,10 +380,11 @@ def main(argv=None):
     slots = max(1, 16 // sharing)
     nmb = max(1, args.multi)                       # batches per launch sequence
     inflight_auto = args.inflight <= 0
-    # small shards want 16 batches in flight, one hardware queue each; a multi-rank run adds the
-    # exchange ring's stream and RCCL's own, and past ~16 user queues the scheduler time-slices
-    # them ("One hardware queue per in-flight slot"), so it keeps 12
-    small_depth = 12 if (world > 1 or force_dist) else 16
+    # small shards want 16 batches in flight, one hardware queue each. A multi-rank run adds the
+    # exchange ring's stream and RCCL's own; it kept 12 for a while (past ~16 user queues the
+    # scheduler time-slices them), but over 160 steps of 2^17 shards 16 beats 12 with the RCCL
+    # loop too: 5.67-5.68e8 against 5.48-5.54e8 (profiles/r06/r06zz4_inflight_s160_n17.log)
+    small_depth = 16
     if args.inflight <= 0:
         if nmb > 1:    # several batches per launch: 3 launches of >= 2^20 items in flight (tools/sweep_multi.sh;
             # union first measured 6.38e8 at 3 and 5.55e8 at 6 at 8 x 2^17, profiles/r04/r04w_union_inflight6_summary.log)

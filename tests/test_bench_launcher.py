@@ -91,7 +91,7 @@ def test_launched_ranks_fail_fast_without_gpus():
 
 def test_default_inflight_by_shard_size():
     """batches in flight per GPU by signatures per GPU: the N = 1 headline (2^20) and the 2-, 4-
-    and 8-rank strong shards (2^19, 2^18, 2^17; small shards keep 12 beside RCCL, 16 alone)"""
+    and 8-rank strong shards (2^19, 2^18, 2^17; small shards keep 16, beside RCCL too)"""
     assert bench.default_inflight(1 << 21, 12) == 6
     assert bench.default_inflight(1 << 20, 16) == 6
     assert bench.default_inflight(1 << 19, 12) == 7
